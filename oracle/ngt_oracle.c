@@ -1,0 +1,514 @@
+/*
+ * ngt_oracle.c -- CPU restatement of the NGT 1.13.8 distance/search hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ngt_oracle.h).  Compiled with
+ * -ffp-contract=off so that every fused multiply-add below is the explicit
+ * fmaf() that mirrors the reference's `vfmadd231ps` and nothing else is
+ * contracted.
+ */
+#include "ngt_oracle.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------- */
+/* Float reductions as emitted by the reference's AVX-512 build.             */
+/* ------------------------------------------------------------------------- */
+
+/* 16 lanes -> 8 -> 4 (lane j + lane j+8, then j + j+4), then
+ * (x0+x1)+(x2+x3).  Matches the vextractf32x8/vextractf128/vunpckhps/vshufps
+ * sequence of ComparatorL2 (PrimitiveComparator.h:154-155,193-196). */
+static float hsum16(const float acc[16]) {
+  float t8[8], t4[4];
+  for (int j = 0; j < 8; j++) t8[j] = acc[j + 8] + acc[j];
+  for (int j = 0; j < 4; j++) t4[j] = t8[j + 4] + t8[j];
+  return (t4[0] + t4[1]) + (t4[2] + t4[3]);
+}
+
+/* PrimitiveComparator::compareL2(const float*, ...) (PrimitiveComparator.h:143-198):
+ * AVX-512 16-lane accumulate of (a-b)^2 with FMA, tree reduce, sqrt in double. */
+static double l2_f32(const float *a, const float *b, size_t n) {
+  float acc[16] = {0};
+  for (size_t i = 0; i < n; i += 16)
+    for (int j = 0; j < 16; j++) {
+      float v = a[i + j] - b[i + j];
+      acc[j] = fmaf(v, v, acc[j]);
+    }
+  return sqrt((double)hsum16(acc));
+}
+
+/* PrimitiveComparator::compareL1(const float*, ...) (PrimitiveComparator.h:269-289):
+ * 8-lane AVX sum of |a-b| (no FMA), horizontal ((x0+x1)+(x2+x3))+((x4+x5)+(x6+x7)). */
+static double l1_f32(const float *a, const float *b, size_t n) {
+  float acc[8] = {0};
+  size_t i = 0;
+  for (; i + 7 < n; i += 8)
+    for (int j = 0; j < 8; j++) acc[j] = acc[j] + fabsf(a[i + j] - b[i + j]);
+  double s = (double)(((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+                      ((acc[4] + acc[5]) + (acc[6] + acc[7])));
+  for (; i < n; i++) s += fabs((double)(a[i] - b[i]));
+  return s;
+}
+
+/* PrimitiveComparator::compareDotProduct(const float*, ...) (PrimitiveComparator.h:446-477):
+ * 16-lane FMA, 16->8->4 in float, final four lanes summed in double. */
+static double dot_f32(const float *a, const float *b, size_t n) {
+  float acc[16] = {0};
+  for (size_t i = 0; i < n; i += 16)
+    for (int j = 0; j < 16; j++) acc[j] = fmaf(b[i + j], a[i + j], acc[j]);
+  float t8[8], t4[4];
+  for (int j = 0; j < 8; j++) t8[j] = acc[j + 8] + acc[j];
+  for (int j = 0; j < 4; j++) t4[j] = t8[j + 4] + t8[j];
+  return ((double)t4[0] + (double)t4[1]) + ((double)t4[2] + (double)t4[3]);
+}
+
+/* PrimitiveComparator::compareCosine(const float*, ...) (PrimitiveComparator.h:487-553). */
+static double cosine_f32(const float *a, const float *b, size_t n) {
+  float na[16] = {0}, nb[16] = {0}, s[16] = {0};
+  for (size_t i = 0; i < n; i += 16)
+    for (int j = 0; j < 16; j++) {
+      na[j] = fmaf(a[i + j], a[i + j], na[j]);
+      nb[j] = fmaf(b[i + j], b[i + j], nb[j]);
+      s[j] = fmaf(b[i + j], a[i + j], s[j]);
+    }
+  double dna = hsum16(na), dnb = hsum16(nb), ds = hsum16(s);
+  return ds / sqrt(dna * dnb);
+}
+
+/* compareAngleDistance / compareNormalizedAngleDistance (PrimitiveComparator.h:571-593). */
+static double angle_of(double c) {
+  if (c >= 1.0) return 0.0;
+  if (c <= -1.0) return acos(-1.0);
+  return acos(c);
+}
+
+/* PrimitiveComparator::compareSparseJaccardDistance(const float*, ...)
+ * (PrimitiveComparator.h:399-418) -- including the reference's use of
+ * bi[loca] in the loop guard. */
+static double sparse_jaccard_f32(const float *a, const float *b, size_t size) {
+  size_t loca = 0, locb = 0, count = 0;
+  const uint32_t *ai = (const uint32_t *)a, *bi = (const uint32_t *)b;
+  while (locb < size && ai[loca] != 0 && bi[loca] != 0) {
+    int64_t sub = (int64_t)ai[loca] - (int64_t)bi[locb];
+    count += sub == 0;
+    loca += sub <= 0;
+    locb += sub >= 0;
+  }
+  while (ai[loca] != 0) loca++;
+  while (locb < size && bi[locb] != 0) locb++;
+  return 1.0 - (double)count / (double)(loca + locb - count);
+}
+
+/* comparePoincareDistance(const float*) (PrimitiveComparator.h:608-618). */
+static double poincare_f32(const float *a, const float *b, size_t n) {
+  double a2 = 0.0, b2 = 0.0, c2 = l2_f32(a, b, n);
+  for (size_t i = 0; i < n; i++) {
+    a2 += (double)a[i] * (double)a[i];
+    b2 += (double)b[i] * (double)b[i];
+  }
+  return acosh(1 + 2.0 * c2 * c2 / (1.0 - a2) / (1.0 - b2));
+}
+
+/* compareLorentzDistance(const float*) (PrimitiveComparator.h:630-637). */
+static double lorentz_f32(const float *a, const float *b, size_t n) {
+  double sum = (double)a[0] * (double)b[0];
+  for (size_t i = 1; i < n; i++) sum -= (double)a[i] * (double)b[i];
+  return acosh(sum);
+}
+
+/* ------------------------------------------------------------------------- */
+/* uint8 comparators (exact integer arithmetic in float/double lanes).       */
+/* ------------------------------------------------------------------------- */
+
+/* compareL2(const unsigned char*, ...) (PrimitiveComparator.h:200-223): squares
+ * of 16-bit differences summed in 4 float lanes (lane c takes elements c and
+ * c+4 of each 8-byte group; -Ofast pairs them first), horizontal
+ * (x0+x1)+(x2+x3), tail in double, sqrt. */
+static double l2_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  float acc[4] = {0};
+  size_t i = 0;
+  for (; i + 7 < n; i += 8)
+    for (int c = 0; c < 4; c++) {
+      int d0 = (int)a[i + c] - (int)b[i + c], d1 = (int)a[i + c + 4] - (int)b[i + c + 4];
+      acc[c] = acc[c] + ((float)(d0 * d0) + (float)(d1 * d1));
+    }
+  double s = (double)((acc[0] + acc[1]) + (acc[2] + acc[3]));
+  for (; i < n; i++) {
+    int d = (int)a[i] - (int)b[i];
+    s += d * d;
+  }
+  return sqrt(s);
+}
+
+/* compareL1(const unsigned char*, ...) (PrimitiveComparator.h:290-313). */
+static double l1_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  float acc[4] = {0};
+  size_t i = 0;
+  for (; i + 7 < n; i += 8)
+    for (int c = 0; c < 4; c++) {
+      int d0 = abs((int)a[i + c] - (int)b[i + c]), d1 = abs((int)a[i + c + 4] - (int)b[i + c + 4]);
+      acc[c] = acc[c] + ((float)d0 + (float)d1);
+    }
+  double s = (double)((acc[0] + acc[1]) + (acc[2] + acc[3]));
+  for (; i < n; i++) s += fabs((double)a[i] - (double)b[i]);
+  return s;
+}
+
+/* compareHammingDistance (PrimitiveComparator.h:340-353): popcount over u64 words. */
+static double hamming_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  size_t count = 0;
+  for (size_t i = 0; i + 8 <= n; i += 8) {
+    uint64_t x, y;
+    memcpy(&x, a + i, 8);
+    memcpy(&y, b + i, 8);
+    count += (size_t)__builtin_popcountll(x ^ y);
+  }
+  return (double)count;
+}
+
+/* compareJaccardDistance (PrimitiveComparator.h:375-391). */
+static double jaccard_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  size_t count = 0, de = 0;
+  for (size_t i = 0; i + 8 <= n; i += 8) {
+    uint64_t x, y;
+    memcpy(&x, a + i, 8);
+    memcpy(&y, b + i, 8);
+    count += (size_t)__builtin_popcountll(x & y);
+    de += (size_t)__builtin_popcountll(x | y);
+  }
+  return 1.0 - (double)count / (double)de;
+}
+
+/* compareDotProduct / compareCosine on uint8 (PrimitiveComparator.h:479-485, 555-568):
+ * double sums of exact integer products, order-independent. */
+static double dot_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  double s = 0.0;
+  for (size_t i = 0; i < n; i++) s += (double)a[i] * (double)b[i];
+  return s;
+}
+static double cosine_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  double na = 0.0, nb = 0.0, s = 0.0;
+  for (size_t i = 0; i < n; i++) {
+    na += (double)a[i] * (double)a[i];
+    nb += (double)b[i] * (double)b[i];
+    s += (double)a[i] * (double)b[i];
+  }
+  return s / sqrt(na * nb);
+}
+static double poincare_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  double a2 = 0.0, b2 = 0.0, c2 = l2_u8(a, b, n);
+  for (size_t i = 0; i < n; i++) {
+    a2 += (double)a[i] * (double)a[i];
+    b2 += (double)b[i] * (double)b[i];
+  }
+  return acosh(1 + 2.0 * c2 * c2 / (1.0 - a2) / (1.0 - b2));
+}
+static double lorentz_u8(const uint8_t *a, const uint8_t *b, size_t n) {
+  double sum = (double)a[0] * (double)b[0];
+  for (size_t i = 1; i < n; i++) sum -= (double)a[i] * (double)b[i];
+  return acosh(sum);
+}
+
+/* ObjectSpaceRepository::setDistanceType (ObjectSpaceRepository.h:346-441)
+ * dispatch, for both object types. */
+static double compare(int metric, int otype, const void *pa, const void *pb, size_t dp) {
+  if (otype == NGTO_FLOAT) {
+    const float *a = (const float *)pa, *b = (const float *)pb;
+    switch (metric) {
+      case NGTO_L1: return l1_f32(a, b, dp);
+      case NGTO_L2: return l2_f32(a, b, dp);
+      case NGTO_ANGLE: return angle_of(cosine_f32(a, b, dp));
+      case NGTO_COSINE: return 1.0 - cosine_f32(a, b, dp);
+      case NGTO_NORMALIZED_ANGLE: return angle_of(dot_f32(a, b, dp));
+      case NGTO_NORMALIZED_COSINE: {
+        double v = 1.0 - dot_f32(a, b, dp);
+        return v < 0.0 ? 0.0 : v;
+      }
+      case NGTO_NORMALIZED_L2: {
+        double v = 2.0 - 2.0 * dot_f32(a, b, dp);
+        return v < 0.0 ? 0.0 : sqrt(v);
+      }
+      case NGTO_SPARSE_JACCARD: return sparse_jaccard_f32(a, b, dp);
+      case NGTO_POINCARE: return poincare_f32(a, b, dp);
+      case NGTO_LORENTZ: return lorentz_f32(a, b, dp);
+      case NGTO_HAMMING: return hamming_u8((const uint8_t *)pa, (const uint8_t *)pb, dp);
+      case NGTO_JACCARD: return jaccard_u8((const uint8_t *)pa, (const uint8_t *)pb, dp);
+      default: return l2_f32(a, b, dp);
+    }
+  } else {
+    const uint8_t *a = (const uint8_t *)pa, *b = (const uint8_t *)pb;
+    switch (metric) {
+      case NGTO_L1: return l1_u8(a, b, dp);
+      case NGTO_L2: return l2_u8(a, b, dp);
+      case NGTO_HAMMING: return hamming_u8(a, b, dp);
+      case NGTO_JACCARD: return jaccard_u8(a, b, dp);
+      case NGTO_ANGLE: return angle_of(cosine_u8(a, b, dp));
+      case NGTO_COSINE: return 1.0 - cosine_u8(a, b, dp);
+      case NGTO_NORMALIZED_ANGLE: return angle_of(dot_u8(a, b, dp));
+      case NGTO_NORMALIZED_COSINE: {
+        double v = 1.0 - dot_u8(a, b, dp);
+        return v < 0.0 ? 0.0 : v;
+      }
+      case NGTO_NORMALIZED_L2: {
+        double v = 2.0 - 2.0 * dot_u8(a, b, dp);
+        return v < 0.0 ? 0.0 : sqrt(v);
+      }
+      case NGTO_POINCARE: return poincare_u8(a, b, dp);
+      case NGTO_LORENTZ: return lorentz_u8(a, b, dp);
+      default: return l2_u8(a, b, dp);
+    }
+  }
+}
+
+float ngto_distance(int metric, int otype, const void *a, const void *b, size_t dp) {
+  return (float)compare(metric, otype, a, b, dp);
+}
+
+void ngto_distances(int metric, int otype, const void *query, const void *rows,
+                    size_t row_bytes, const uint32_t *ids, size_t n, size_t dp,
+                    float *out) {
+  for (size_t i = 0; i < n; i++)
+    out[i] = ngto_distance(metric, otype, query,
+                           (const uint8_t *)rows + (size_t)ids[i] * row_bytes, dp);
+}
+
+/* ObjectSpace::normalize<float> (ObjectSpace.h:251-266). */
+int ngto_normalize_f32(float *v, size_t dim) {
+  float sum = 0.0f;
+  for (size_t i = 0; i < dim; i++) sum += v[i] * v[i];
+  if (sum == 0.0f) return -1;
+  sum = sqrtf(sum);
+  for (size_t i = 0; i < dim; i++) v[i] = v[i] / sum;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* (distance, id) heaps -- ObjectDistance ordering (Common.h:1946-1959).      */
+/* ------------------------------------------------------------------------- */
+
+typedef struct { uint32_t id; float d; } od_t;
+
+static int od_less(od_t x, od_t y) { return x.d == y.d ? x.id < y.id : x.d < y.d; }
+
+typedef struct { od_t *v; size_t n, cap; int max_heap; } heap_t;
+
+static int heap_before(const heap_t *h, od_t x, od_t y) {
+  return h->max_heap ? od_less(y, x) : od_less(x, y);
+}
+static void heap_push(heap_t *h, od_t x) {
+  if (h->n == h->cap) {
+    h->cap = h->cap ? h->cap * 2 : 64;
+    h->v = (od_t *)realloc(h->v, h->cap * sizeof(od_t));
+  }
+  size_t i = h->n++;
+  while (i > 0) {
+    size_t p = (i - 1) / 2;
+    if (!heap_before(h, x, h->v[p])) break;
+    h->v[i] = h->v[p];
+    i = p;
+  }
+  h->v[i] = x;
+}
+static od_t heap_pop(heap_t *h) {
+  od_t top = h->v[0], x = h->v[--h->n];
+  size_t i = 0;
+  for (;;) {
+    size_t c = 2 * i + 1;
+    if (c >= h->n) break;
+    if (c + 1 < h->n && heap_before(h, h->v[c + 1], h->v[c])) c++;
+    if (!heap_before(h, h->v[c], x)) break;
+    h->v[i] = h->v[c];
+    i = c;
+  }
+  if (h->n) h->v[i] = x;
+  return top;
+}
+
+static int od_cmp(const void *pa, const void *pb) {
+  od_t a = *(const od_t *)pa, b = *(const od_t *)pb;
+  return od_less(a, b) ? -1 : (od_less(b, a) ? 1 : 0);
+}
+
+/* Drain a max-heap into ascending order: ObjectDistances::moveFrom
+ * (ObjectSpace.h:49-57). */
+static int drain(heap_t *res, uint32_t *ids, float *dists) {
+  int n = (int)res->n;
+  for (int i = n - 1; i >= 0; i--) {
+    od_t t = heap_pop(res);
+    ids[i] = t.id;
+    dists[i] = t.d;
+  }
+  return n;
+}
+
+int ngto_search(int metric, int otype, const void *rows, size_t row_bytes,
+                size_t nrows, size_t dp, const uint64_t *edge_off,
+                const uint32_t *edge_ids, const void *query,
+                const uint32_t *seeds, size_t nseeds, size_t k, float epsilon,
+                float radius_in, size_t edge_size, uint32_t *out_ids,
+                float *out_dists, uint64_t *counters) {
+  const uint8_t *base = (const uint8_t *)rows;
+  /* SearchContainer::setEpsilon (Common.h:2041) and the 0 => 1.1 default
+   * (Graph.cpp:403-405). */
+  float coef = (float)((double)epsilon + 1.0);
+  if (coef == 0.0f) coef = (float)1.1;
+  float radius = radius_in;
+  if (edge_size == 0) edge_size = (size_t)INT_MAX;
+  uint64_t ndist = 0, nvisit = 0, nexp = 0;
+  if (k == 0) { if (counters) counters[0] = counters[1] = counters[2] = 0; return 0; }
+
+  uint8_t *checked = (uint8_t *)calloc(nrows, 1);
+  heap_t unchecked = {0, 0, 0, 0}, results = {0, 0, 0, 1};
+
+  /* setupDistances (Graph.cpp:293-338) + setupSeeds (Graph.cpp:341-367). */
+  od_t *sd = (od_t *)malloc((nseeds ? nseeds : 1) * sizeof(od_t));
+  for (size_t i = 0; i < nseeds; i++) {
+    sd[i].id = seeds[i];
+    sd[i].d = ngto_distance(metric, otype, query, base + (size_t)seeds[i] * row_bytes, dp);
+  }
+  ndist += nseeds;
+  qsort(sd, nseeds, sizeof(od_t), od_cmp);
+  for (size_t i = 0; i < nseeds; i++) {
+    if (results.n < k && sd[i].d <= radius) heap_push(&results, sd[i]);
+    else break;
+  }
+  if (results.n >= k) radius = results.v[0].d;
+  for (size_t i = 0; i < nseeds; i++) {
+    checked[sd[i].id] = 1;
+    heap_push(&unchecked, sd[i]);
+  }
+  free(sd);
+
+  /* The best-first loop (Graph.cpp:420-486). */
+  float expr = coef * radius;
+  uint32_t *ns = NULL;
+  size_t ns_cap = 0;
+  while (unchecked.n) {
+    od_t target = heap_pop(&unchecked);
+    if (target.d > expr) break;
+    nexp++;
+    uint64_t beg = edge_off[target.id], end = edge_off[target.id + 1];
+    size_t deg = (size_t)(end - beg);
+    if (deg > edge_size) deg = edge_size;
+    if (deg > ns_cap) { ns_cap = deg; ns = (uint32_t *)realloc(ns, ns_cap * sizeof(uint32_t)); }
+    size_t nns = 0;
+    for (size_t e = 0; e < deg; e++)
+      if (!checked[edge_ids[beg + e]]) ns[nns++] = edge_ids[beg + e];
+    for (size_t i = 0; i < nns; i++) {
+      uint32_t id = ns[i];
+      nvisit++;
+      checked[id] = 1;
+      ndist++;
+      float d = ngto_distance(metric, otype, query, base + (size_t)id * row_bytes, dp);
+      if (d <= expr) {
+        od_t r = {id, d};
+        heap_push(&unchecked, r);
+        if (d <= radius) {
+          heap_push(&results, r);
+          if (results.n >= k) {
+            if (results.n > k) heap_pop(&results);
+            radius = results.v[0].d;
+            expr = coef * radius;
+          }
+        }
+      }
+    }
+  }
+  int n = drain(&results, out_ids, out_dists);
+  free(ns);
+  free(unchecked.v);
+  free(results.v);
+  free(checked);
+  if (counters) {
+    counters[0] = ndist;
+    counters[1] = nvisit;
+    counters[2] = nexp;
+  }
+  return n;
+}
+
+int ngto_linear_search(int metric, int otype, const void *rows, size_t row_bytes,
+                       size_t nrows, size_t dp, const uint8_t *valid,
+                       const void *query, size_t k, double radius,
+                       uint32_t *out_ids, float *out_dists) {
+  heap_t results = {0, 0, 0, 1};
+  const uint8_t *base = (const uint8_t *)rows;
+  for (size_t idx = 1; idx < nrows; idx++) {
+    if (valid && !valid[idx]) continue;
+    float d = ngto_distance(metric, otype, query, base + idx * row_bytes, dp);
+    if (radius < 0.0 || d <= radius) {
+      od_t r = {(uint32_t)idx, d};
+      heap_push(&results, r);
+      if (results.n > k) heap_pop(&results);
+    }
+  }
+  int n = drain(&results, out_ids, out_dists);
+  free(results.v);
+  return n;
+}
+
+/* glibc srandom_r / random_r for TYPE_3 (degree 31, separation 3). */
+void ngto_srand(ngto_rand_t *g, unsigned seed) {
+  int32_t word = (int32_t)(seed == 0 ? 1 : seed);
+  g->s[0] = (uint32_t)word;
+  for (int i = 1; i < 31; i++) {
+    int32_t hi = word / 127773, lo = word % 127773;
+    word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    g->s[i] = (uint32_t)word;
+  }
+  g->f = 3;
+  g->r = 0;
+  for (int i = 0; i < 310; i++) ngto_rand(g);
+}
+
+int ngto_rand(ngto_rand_t *g) {
+  g->s[g->f] += g->s[g->r];
+  int res = (int)((g->s[g->f] >> 1) & 0x7fffffff);
+  g->f = (g->f + 1) % 31;
+  g->r = (g->r + 1) % 31;
+  return res;
+}
+
+size_t ngto_thin_seeds(uint32_t *seeds, size_t n, unsigned leaf_id,
+                       size_t seed_size, size_t k) {
+  size_t ss = seed_size == 0 ? k : seed_size;
+  if (ss > k) ss = k;
+  if (n > ss) {
+    ngto_rand_t g;
+    ngto_srand(&g, leaf_id);
+    for (size_t i = n; i > ss; i--) {
+      double random = ((double)ngto_rand(&g) + 1.0) / ((double)RAND_MAX + 2.0);
+      size_t idx = (size_t)floor((double)i * random);
+      seeds[idx] = seeds[i - 1];
+    }
+    return ss;
+  }
+  return n;
+}
+
+uint32_t ngto_tree_leaf(int metric, int otype, const void *query, size_t dp,
+                        uint32_t root, const void *in_pivot, size_t row_bytes,
+                        const uint32_t *in_child, const float *in_border,
+                        size_t children, uint64_t *ndist) {
+  uint32_t node = root;
+  uint64_t nd = 0;
+  while (!(node & 0x80000000u)) {
+    uint32_t iid = node & 0x7fffffffu;
+    float d = ngto_distance(metric, otype, query,
+                            (const uint8_t *)in_pivot + (size_t)iid * row_bytes, dp);
+    nd++;
+    const float *borders = in_border + (size_t)iid * (children - 1);
+    size_t mid;
+    /* radius = 0: the first region with d < border, else the last one
+     * (Tree.cpp:424-456, regions sorted, front taken at :468). */
+    for (mid = 0; mid < children - 1; mid++)
+      if (d < borders[mid]) break;
+    node = in_child[(size_t)iid * children + mid];
+  }
+  if (ndist) *ndist = nd;
+  return node;
+}

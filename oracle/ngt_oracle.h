@@ -1,0 +1,97 @@
+/*
+ * ngt_oracle.h -- CPU restatement of NGT 1.13.8's distance / search hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the *checker* for the HIP
+ * product path in ngt_amd/.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product never links it and
+ * never falls back to it.
+ *
+ * Every function restates the reference algorithm and cites the reference
+ * file:line it follows (paths relative to the reference repository root).
+ * The float reduction orders were read off the AVX-512 build of the
+ * reference (`-Ofast -march=native`, objdump of
+ * ObjectSpaceRepository<float,double>::Comparator*::operator()) and are pinned
+ * bit-exactly by tests/golden (edge distances stored in reference-built
+ * `grp` files).
+ */
+#ifndef NGT_ORACLE_H
+#define NGT_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* NGT::ObjectSpace::DistanceType (lib/NGT/ObjectSpace.h:166-180) */
+enum {
+  NGTO_L1 = 0, NGTO_L2 = 1, NGTO_HAMMING = 2, NGTO_ANGLE = 3, NGTO_COSINE = 4,
+  NGTO_NORMALIZED_ANGLE = 5, NGTO_NORMALIZED_COSINE = 6, NGTO_JACCARD = 7,
+  NGTO_SPARSE_JACCARD = 8, NGTO_NORMALIZED_L2 = 9, NGTO_POINCARE = 100,
+  NGTO_LORENTZ = 101
+};
+/* NGT::ObjectSpace::ObjectType (lib/NGT/ObjectSpace.h:182-186) */
+enum { NGTO_UINT8 = 1, NGTO_FLOAT = 2 };
+
+/* One comparator call, returned as the float the callers store
+ * (Distance = float, lib/NGT/Common.h:47).  a, b point at padded rows of
+ * `dp` elements (zero padded, lib/NGT/ObjectSpace.h:392-397). */
+float ngto_distance(int metric, int otype, const void *a, const void *b, size_t dp);
+
+/* Batched form: out[i] = distance(query, rows + ids[i]*row_bytes). */
+void ngto_distances(int metric, int otype, const void *query, const void *rows,
+                    size_t row_bytes, const uint32_t *ids, size_t n, size_t dp,
+                    float *out);
+
+/* NGT::ObjectSpace::normalize (lib/NGT/ObjectSpace.h:251-266) on a float row. */
+int ngto_normalize_f32(float *v, size_t dim);
+
+/* NeighborhoodGraph::searchReadOnlyGraph<COMPARATOR, CHECK_LIST>
+ * (lib/NGT/Graph.cpp:398-495) with setupDistances (:293-338) and setupSeeds
+ * (:341-367).  Graph is CSR: edges of node v are edge_ids[edge_off[v] ..
+ * edge_off[v+1]).  `edge_size` is the already-resolved getEdgeSize()
+ * (lib/NGT/Graph.h:675-692; 0 or INT_MAX = unlimited).
+ * Returns the number of results (<= k) written to out_ids/out_dists in
+ * ascending (distance, id) order; counters[0] = distance computations,
+ * counters[1] = visited edges, counters[2] = expansions. */
+int ngto_search(int metric, int otype, const void *rows, size_t row_bytes,
+                size_t nrows, size_t dp, const uint64_t *edge_off,
+                const uint32_t *edge_ids, const void *query,
+                const uint32_t *seeds, size_t nseeds, size_t k, float epsilon,
+                float radius, size_t edge_size, uint32_t *out_ids,
+                float *out_dists, uint64_t *counters);
+
+/* ObjectSpaceRepository::linearSearch (lib/NGT/ObjectSpaceRepository.h:466-502):
+ * all rows 1..nrows-1 whose valid[i] != 0 (valid may be NULL). */
+int ngto_linear_search(int metric, int otype, const void *rows, size_t row_bytes,
+                       size_t nrows, size_t dp, const uint8_t *valid,
+                       const void *query, size_t k, double radius,
+                       uint32_t *out_ids, float *out_dists);
+
+/* glibc random(3) TYPE_3 restatement, used by getSeedsFromTree's
+ * srand(leafID) thinning (lib/NGT/Index.h:1555-1561) and getRandomSeeds
+ * (lib/NGT/Index.h:775-801). */
+typedef struct { uint32_t s[31]; int f, r; } ngto_rand_t;
+void ngto_srand(ngto_rand_t *g, unsigned seed);
+int ngto_rand(ngto_rand_t *g);
+
+/* GraphAndTreeIndex::getSeedsFromTree seed thinning (lib/NGT/Index.h:1548-1566):
+ * seeds (leaf object ids, in leaf order) are thinned in place to
+ * min(seed_size==0?k:seed_size, k) using srand(leaf_id).  Returns new count. */
+size_t ngto_thin_seeds(uint32_t *seeds, size_t n, unsigned leaf_id,
+                       size_t seed_size, size_t k);
+
+/* DVPTree::search in SearchLeaf mode with radius 0 (lib/NGT/Tree.cpp:400-480,
+ * 531-563).  Tree arrays: internal node i: pivot row `in_pivot + i*row_bytes`,
+ * children in_child[i*5..], borders in_border[i*4..]; node ids follow
+ * Node::ID (bit 31 = leaf).  root = raw ID of the root.  Returns the leaf's
+ * raw node ID; *ndist gets the number of distance computations. */
+uint32_t ngto_tree_leaf(int metric, int otype, const void *query, size_t dp,
+                        uint32_t root, const void *in_pivot, size_t row_bytes,
+                        const uint32_t *in_child, const float *in_border,
+                        size_t children, uint64_t *ndist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

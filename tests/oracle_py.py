@@ -1,0 +1,134 @@
+"""ctypes binding of the CPU restatement in oracle/ (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = None
+
+METRICS = {
+    "l1": 0, "l2": 1, "hamming": 2, "angle": 3, "cosine": 4, "normalized_angle": 5,
+    "normalized_cosine": 6, "jaccard": 7, "sparse_jaccard": 8, "normalized_l2": 9,
+    "poincare": 100, "lorentz": 101,
+}
+OTYPES = {"c": 1, "u8": 1, "f": 2, "f32": 2}
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(ROOT, "oracle", "libngt_oracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(path)
+        vp, sz, u32p, f32p, u64p = (ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_uint32),
+                                    ctypes.POINTER(ctypes.c_float),
+                                    ctypes.POINTER(ctypes.c_uint64))
+        L.ngto_distance.restype = ctypes.c_float
+        L.ngto_distance.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz]
+        L.ngto_distances.restype = None
+        L.ngto_distances.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, u32p, sz, sz, f32p]
+        L.ngto_search.restype = ctypes.c_int
+        L.ngto_search.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, sz, sz, u64p, u32p, vp,
+                                  u32p, sz, sz, ctypes.c_float, ctypes.c_float, sz, u32p, f32p, u64p]
+        L.ngto_linear_search.restype = ctypes.c_int
+        L.ngto_linear_search.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, sz, sz, vp, vp, sz,
+                                         ctypes.c_double, u32p, f32p]
+        L.ngto_thin_seeds.restype = sz
+        L.ngto_thin_seeds.argtypes = [u32p, sz, ctypes.c_uint, sz, sz]
+        L.ngto_tree_leaf.restype = ctypes.c_uint32
+        L.ngto_tree_leaf.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, ctypes.c_uint32, vp, sz,
+                                     u32p, f32p, sz, u64p]
+        L.ngto_normalize_f32.restype = ctypes.c_int
+        L.ngto_normalize_f32.argtypes = [f32p, sz]
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def distances(metric, rows, query, ids):
+    """Reference comparator distances between `query` and rows[ids]."""
+    rows = np.ascontiguousarray(rows)
+    query = np.ascontiguousarray(query, dtype=rows.dtype)
+    ids = np.ascontiguousarray(ids, dtype=np.uint32)
+    out = np.zeros(len(ids), np.float32)
+    ot = 2 if rows.dtype == np.float32 else 1
+    lib().ngto_distances(METRICS[metric], ot, query.ctypes.data, rows.ctypes.data,
+                         rows.strides[0], _p(ids, ctypes.c_uint32), len(ids), rows.shape[1],
+                         _p(out, ctypes.c_float))
+    return out
+
+
+def pair_distances(metric, rows, src, dst):
+    rows = np.ascontiguousarray(rows)
+    ot = 2 if rows.dtype == np.float32 else 1
+    L = lib()
+    out = np.empty(len(src), np.float32)
+    rb = rows.strides[0]
+    base = rows.ctypes.data
+    m = METRICS[metric]
+    for i, (s, d) in enumerate(zip(src, dst)):
+        out[i] = L.ngto_distance(m, ot, base + int(s) * rb, base + int(d) * rb, rows.shape[1])
+    return out
+
+
+def search(metric, rows, offsets, edges, query, seeds, k, epsilon, radius=3.402823466e38,
+           edge_size=0):
+    rows = np.ascontiguousarray(rows)
+    ot = 2 if rows.dtype == np.float32 else 1
+    query = np.ascontiguousarray(query, dtype=rows.dtype)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    edges = np.ascontiguousarray(edges, dtype=np.uint32)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+    ids = np.zeros(max(k, 1), np.uint32)
+    ds = np.zeros(max(k, 1), np.float32)
+    cnt = np.zeros(3, np.uint64)
+    n = lib().ngto_search(METRICS[metric], ot, rows.ctypes.data, rows.strides[0], rows.shape[0],
+                          rows.shape[1], _p(offsets, ctypes.c_uint64), _p(edges, ctypes.c_uint32),
+                          query.ctypes.data, _p(seeds, ctypes.c_uint32), len(seeds), k,
+                          epsilon, radius, edge_size, _p(ids, ctypes.c_uint32),
+                          _p(ds, ctypes.c_float), _p(cnt, ctypes.c_uint64))
+    return ids[:n].copy(), ds[:n].copy(), cnt
+
+
+def linear_search(metric, rows, query, k, valid=None, radius=-1.0):
+    rows = np.ascontiguousarray(rows)
+    ot = 2 if rows.dtype == np.float32 else 1
+    query = np.ascontiguousarray(query, dtype=rows.dtype)
+    ids = np.zeros(max(k, 1), np.uint32)
+    ds = np.zeros(max(k, 1), np.float32)
+    vptr = None
+    if valid is not None:
+        valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        vptr = valid.ctypes.data
+    n = lib().ngto_linear_search(METRICS[metric], ot, rows.ctypes.data, rows.strides[0],
+                                 rows.shape[0], rows.shape[1], vptr, query.ctypes.data, k, radius,
+                                 _p(ids, ctypes.c_uint32), _p(ds, ctypes.c_float))
+    return ids[:n].copy(), ds[:n].copy()
+
+
+def tree_seeds(metric, tree, query, k, seed_size=10, dtype=np.float32):
+    """getSeedsFromTree (lib/NGT/Index.h:1524-1567) on a parsed tre dict."""
+    query = np.ascontiguousarray(query, dtype=dtype)
+    piv = np.ascontiguousarray(tree["in_pivot"])
+    child = np.ascontiguousarray(tree["in_child"], dtype=np.uint32)
+    border = np.ascontiguousarray(tree["in_border"], dtype=np.float32)
+    nd = np.zeros(1, np.uint64)
+    ot = 2 if piv.dtype == np.float32 else 1
+    leaf = lib().ngto_tree_leaf(METRICS[metric], ot, query.ctypes.data, piv.shape[1], tree["root"],
+                                piv.ctypes.data, piv.strides[0], _p(child, ctypes.c_uint32),
+                                _p(border, ctypes.c_float), 5, _p(nd, ctypes.c_uint64))
+    lid = leaf & 0x7FFFFFFF
+    b, e = int(tree["leaf_off"][lid]), int(tree["leaf_off"][lid + 1])
+    seeds = np.ascontiguousarray(tree["leaf_ids"][b:e], dtype=np.uint32).copy()
+    n = lib().ngto_thin_seeds(_p(seeds, ctypes.c_uint32), len(seeds), lid, seed_size, k)
+    return seeds[:n].copy(), int(nd[0]), lid
