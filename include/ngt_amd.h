@@ -1,0 +1,159 @@
+/*
+ * ngt_amd.h -- C ABI of the MI355X-native NGT distance hot path.
+ *
+ * These entry points are the batched device form of the reference's search
+ * path.  Each one names the reference interface it replaces:
+ *
+ *   ngt_amd_search          <- NGT::GraphAndTreeIndex::search(SearchContainer&)
+ *                              (lib/NGT/Index.h:1570-1577) and
+ *                              NGT::Index::searchUsingOnlyGraph (Index.h:479-484),
+ *                              i.e. getSeedsFromTree (Index.h:1524-1567) +
+ *                              NeighborhoodGraph::searchReadOnlyGraph
+ *                              (lib/NGT/Graph.cpp:398-495), for a batch of queries.
+ *   ngt_amd_linear_search   <- NGT::GraphIndex::linearSearch (Index.h:729-749) /
+ *                              ObjectSpaceRepository::linearSearch
+ *                              (lib/NGT/ObjectSpaceRepository.h:466-502).
+ *   ngt_amd_distances       <- PrimitiveComparator::<Metric>::compare
+ *                              (lib/NGT/PrimitiveComparator.h:650-752) over a
+ *                              batch of (query, object id) pairs.
+ *   ngt_amd_index_*         <- the object repository / graph / tree that
+ *                              NGT::Index::open loads (lib/NGT/Index.cpp:92-111),
+ *                              laid out in HBM (padded row-major slab, CSR
+ *                              adjacency, flattened DVP tree).
+ *
+ * The drop-in `ngt_*` C API (include/NGT/Capi.h, same names and signatures as
+ * lib/NGT/Capi.h) is implemented on top of these.
+ *
+ * Conventions: plain pointers and sizes; functions return 0 on success and a
+ * negative value on failure with a message retrievable by
+ * ngt_amd_last_error().  `*_device` variants take device pointers and enqueue
+ * on the given HIP stream (hipStream_t passed as void*); the others take host
+ * pointers and are synchronous.  There is no CPU fallback: without a usable
+ * gfx950 device every compute call fails with an error.
+ */
+#ifndef NGT_AMD_H
+#define NGT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* NGT::ObjectSpace::DistanceType values (lib/NGT/ObjectSpace.h:166-180). */
+#define NGT_AMD_DISTANCE_L1 0
+#define NGT_AMD_DISTANCE_L2 1
+#define NGT_AMD_DISTANCE_HAMMING 2
+#define NGT_AMD_DISTANCE_ANGLE 3
+#define NGT_AMD_DISTANCE_COSINE 4
+#define NGT_AMD_DISTANCE_NORMALIZED_ANGLE 5
+#define NGT_AMD_DISTANCE_NORMALIZED_COSINE 6
+#define NGT_AMD_DISTANCE_JACCARD 7
+#define NGT_AMD_DISTANCE_SPARSE_JACCARD 8
+#define NGT_AMD_DISTANCE_NORMALIZED_L2 9
+#define NGT_AMD_DISTANCE_POINCARE 100
+#define NGT_AMD_DISTANCE_LORENTZ 101
+/* NGT::ObjectSpace::ObjectType (lib/NGT/ObjectSpace.h:182-186). */
+#define NGT_AMD_OBJECT_UINT8 1
+#define NGT_AMD_OBJECT_FLOAT 2
+
+/* Seed providers (NeighborhoodGraph::SeedType, lib/NGT/Graph.h:279-285). */
+#define NGT_AMD_SEED_TREE 0    /* DVP-tree leaf (GraphAndTreeIndex::search)        */
+#define NGT_AMD_SEED_GIVEN 1   /* caller-supplied seed lists (search(sc, seeds))    */
+#define NGT_AMD_SEED_RANDOM 2  /* getRandomSeeds over the process rand() stream     */
+
+typedef struct ngt_amd_index ngt_amd_index;
+
+typedef struct {
+  uint32_t k;            /* SearchContainer::size                                  */
+  float epsilon;         /* SearchContainer::setEpsilon (coef = epsilon + 1)         */
+  float radius;          /* SearchContainer::radius; < 0 => FLT_MAX (Capi.cpp:357)   */
+  int64_t edge_size;     /* SearchContainer::edgeSize: -1 property, 0 all, -2 dyn.   */
+  int32_t seed_mode;     /* NGT_AMD_SEED_*                                          */
+  int32_t all_leaf_nodes;/* SearchContainer::useAllNodesInLeaf                      */
+} ngt_amd_search_params;
+
+/* Per-query counters written by the search (4 x uint64 per query):
+ * [0] distance computations (seeds + evaluated neighbours), [1] evaluated
+ * neighbours (visitCount), [2] expanded nodes, [3] 1 if the visited set spilled
+ * from LDS to the HBM bitmap. */
+#define NGT_AMD_COUNTERS_PER_QUERY 4
+
+const char *ngt_amd_last_error(void);
+int ngt_amd_device_count(void);
+
+/* ---- index ------------------------------------------------------------- */
+int ngt_amd_index_create(ngt_amd_index **out, int device, int distance_type,
+                         int object_type, uint32_t dimension);
+void ngt_amd_index_destroy(ngt_amd_index *index);
+/* Padded dimension ((dim-1)/16+1)*16 (ObjectSpace::getPaddedDimension). */
+uint32_t ngt_amd_index_padded_dimension(const ngt_amd_index *index);
+/* rows: host [nrows][padded_dimension] elements, row 0 the dummy slot;
+ * valid: [nrows] (0 = removed slot) or NULL. */
+int ngt_amd_index_set_objects(ngt_amd_index *index, const void *rows, uint64_t nrows,
+                              const uint8_t *valid);
+/* Device rows already in HBM (row-major padded, row_bytes = padded dim *
+ * element size); the index keeps the pointer, the caller keeps ownership. */
+int ngt_amd_index_set_objects_device(ngt_amd_index *index, const void *d_rows, uint64_t nrows);
+/* CSR adjacency: edges of node v are edges[offsets[v] .. offsets[v+1]). */
+int ngt_amd_index_set_graph(ngt_amd_index *index, const uint64_t *offsets,
+                            const uint32_t *edges, uint64_t nedges);
+int ngt_amd_index_set_graph_device(ngt_amd_index *index, const uint64_t *d_offsets,
+                                   const uint32_t *d_edges, uint64_t nedges);
+/* Flattened DVP tree (lib/NGT/Tree.h, Node.h): internal node i has pivot row
+ * in_pivot[i] (padded), children in_child[i*children..], borders
+ * in_border[i*(children-1)..]; leaf j holds leaf_ids[leaf_off[j]..leaf_off[j+1]).
+ * root is the raw Node::ID (bit 31 = leaf). */
+int ngt_amd_index_set_tree(ngt_amd_index *index, const void *in_pivot, uint32_t n_internal,
+                           const uint32_t *in_child, const float *in_border, uint32_t children,
+                           uint32_t root, const uint64_t *leaf_off, uint32_t n_leaf,
+                           const uint32_t *leaf_ids, uint64_t n_leaf_ids);
+/* Graph/search properties (NeighborhoodGraph::Property, lib/NGT/Graph.h:383-524). */
+int ngt_amd_index_set_search_property(ngt_amd_index *index, int32_t edge_size_for_search,
+                                      int32_t dynamic_edge_size_base,
+                                      int32_t dynamic_edge_size_rate, int32_t seed_size,
+                                      int32_t seed_type);
+/* Resolve NeighborhoodGraph::getEdgeSize (lib/NGT/Graph.h:675-692). */
+uint64_t ngt_amd_resolve_edge_size(const ngt_amd_index *index, int64_t edge_size, float epsilon);
+
+/* ---- search ------------------------------------------------------------ */
+/* Host pointers.  queries: [nq][dimension] floats for every object type; they
+ * are converted/normalized on the device exactly like Index::allocateObject.  seeds /
+ * seed_off: CSR seed lists for NGT_AMD_SEED_GIVEN (else NULL).  Outputs:
+ * ids/dists [nq][k] ascending (distance, id), n [nq], counters [nq][4] or NULL. */
+int ngt_amd_search(ngt_amd_index *index, const ngt_amd_search_params *params,
+                   const void *queries, uint32_t nq, const uint32_t *seeds,
+                   const uint64_t *seed_off, uint32_t *ids, float *dists, uint32_t *n,
+                   uint64_t *counters);
+/* Device pointers; queries are already padded rows of the object type
+ * (query_bytes apart) and already normalized where the metric requires it. */
+int ngt_amd_search_device(ngt_amd_index *index, const ngt_amd_search_params *params,
+                          const void *d_queries, uint64_t query_bytes, uint32_t nq,
+                          const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,
+                          float *d_dists, uint32_t *d_n, uint64_t *d_counters, void *stream);
+
+int ngt_amd_linear_search(ngt_amd_index *index, const void *queries, uint32_t nq, uint32_t k,
+                          double radius, uint32_t *ids, float *dists, uint32_t *n);
+int ngt_amd_linear_search_device(ngt_amd_index *index, const void *d_queries,
+                                 uint64_t query_bytes, uint32_t nq, uint32_t k, double radius,
+                                 uint32_t *d_ids, float *d_dists, uint32_t *d_n, void *stream);
+
+/* Pairwise comparator: out[i] = distance(queries[qidx[i]], object oid[i]).
+ * queries are prepared objects ([nq][padded dim] of the object type, as stored). */
+int ngt_amd_distances(ngt_amd_index *index, const void *queries, uint32_t nq,
+                      const uint32_t *qidx, const uint32_t *oid, uint64_t npairs, float *out);
+
+/* Prepare queries on the device exactly like Index::allocateObject: convert
+ * to the object type, zero-pad to the padded dimension, normalize for the
+ * normalized metrics (ObjectSpace::normalize, lib/NGT/ObjectSpace.h:251-266). */
+int ngt_amd_prepare_queries_device(ngt_amd_index *index, const float *d_in, uint32_t nq,
+                                   void *d_out, void *stream);
+
+/* Timing of the last search call's kernels (HIP events on the search stream), ms. */
+float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

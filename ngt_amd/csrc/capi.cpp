@@ -1,0 +1,792 @@
+// capi.cpp -- the reference's `ngt_*` C API (lib/NGT/Capi.cpp) served by the
+// MI355X path.  An NGTIndex is a host mirror of the index files (needed for
+// ngt_get_object_as_float's borrowed pointers, Capi.cpp:750-765, and for
+// ngt_save_index) plus a device-resident ngt_amd_index that every search and
+// linear search runs on.  Error convention of Capi.cpp:25-38.
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/NGT/Capi.h"
+#include "../../include/ngt_amd.h"
+#include "index_io.h"
+
+using ngt_amd::HostIndex;
+using ngt_amd::HostProperty;
+
+namespace {
+
+struct CapiIndex {
+  HostIndex host;
+  ngt_amd_index* dev = nullptr;
+  bool device_stale = true;
+  uint64_t last_counters[3] = {0, 0, 0};
+  ~CapiIndex() {
+    if (dev) ngt_amd_index_destroy(dev);
+  }
+};
+
+typedef std::vector<NGTObjectDistance> Results;
+
+bool set_error(NGTError error, const char* func, const std::string& what) {
+  std::stringstream ss;
+  ss << "Capi : " << func << "() : Error: " << what;
+  if (error != NULL) {
+    *static_cast<std::string*>(error) = ss.str();
+  } else {
+    std::cerr << ss.str() << std::endl;
+  }
+  return true;
+}
+
+bool param_error(NGTError error, const char* func, const std::string& what) {
+  std::stringstream ss;
+  ss << "Capi : " << func << "() : parametor error: " << what;
+  if (error != NULL) {
+    *static_cast<std::string*>(error) = ss.str();
+  } else {
+    std::cerr << ss.str() << std::endl;
+  }
+  return true;
+}
+
+std::string amd_err() { return std::string(ngt_amd_last_error()); }
+
+// Build / refresh the device index from the host mirror.
+std::string sync_device(CapiIndex* ix) {
+  if (!ix->device_stale && ix->dev) return "";
+  HostIndex& h = ix->host;
+  if (h.nrows < 2) return "the index is empty";
+  if (!ix->dev) {
+    int dev = 0;
+    const char* env = getenv("NGT_AMD_DEVICE");
+    if (env) dev = atoi(env);
+    if (ngt_amd_index_create(&ix->dev, dev, h.prop.distance_type, h.prop.object_type,
+                             (uint32_t)h.prop.dimension))
+      return amd_err();
+  }
+  if (ngt_amd_index_set_objects(ix->dev, h.rows.data(), h.nrows, h.valid.data())) return amd_err();
+  if (h.edge_off.size() == h.nrows + 1 && !h.edges.empty()) {
+    if (ngt_amd_index_set_graph(ix->dev, h.edge_off.data(), h.edges.data(), h.edges.size()))
+      return amd_err();
+  }
+  if (h.tree.present) {
+    const ngt_amd::HostTree& t = h.tree;
+    if (ngt_amd_index_set_tree(ix->dev, t.in_pivot.data(), t.n_internal(), t.in_child.data(),
+                               t.in_border.data(), 5, t.root, t.leaf_off.data(), t.n_leaf(),
+                               t.leaf_ids.data(), t.leaf_ids.size()))
+      return amd_err();
+  }
+  ngt_amd_index_set_search_property(ix->dev, h.prop.edge_size_for_search, h.prop.dynamic_edge_size_base,
+                                    h.prop.dynamic_edge_size_rate, h.prop.seed_size, h.prop.seed_type);
+  ix->device_stale = false;
+  return "";
+}
+
+bool use_tree(CapiIndex* ix) { return ix->host.prop.index_type == 0 && ix->host.tree.present; }
+
+// One batched search: the single-query API is a batch of one.
+std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t size, float epsilon,
+                       float radius, int64_t edge_size, int seed_mode, std::vector<uint32_t>& ids,
+                       std::vector<float>& dists, std::vector<uint32_t>& n) {
+  std::string e = sync_device(ix);
+  if (!e.empty()) return e;
+  if (size == 0) {
+    // GraphIndex::search with sc.size == 0 returns nothing (Index.h:1141-1144)
+    n.assign(nq, 0);
+    return "";
+  }
+  ngt_amd_search_params p{};
+  p.k = (uint32_t)size;
+  p.epsilon = epsilon;
+  p.radius = radius < 0.0f ? FLT_MAX : radius;
+  p.edge_size = edge_size;
+  p.seed_mode = seed_mode;
+  p.all_leaf_nodes = 0;
+  ids.resize((size_t)nq * size);
+  dists.resize((size_t)nq * size);
+  n.resize(nq);
+  std::vector<uint64_t> cnt((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY);
+  if (ngt_amd_search(ix->dev, &p, queries, nq, nullptr, nullptr, ids.data(), dists.data(), n.data(),
+                     cnt.data()))
+    return amd_err();
+  ix->last_counters[0] = ix->last_counters[1] = ix->last_counters[2] = 0;
+  for (uint32_t q = 0; q < nq; q++)
+    for (int c = 0; c < 3; c++) ix->last_counters[c] += cnt[(size_t)q * NGT_AMD_COUNTERS_PER_QUERY + c];
+  return "";
+}
+
+std::string run_linear(CapiIndex* ix, const float* queries, uint32_t nq, size_t size,
+                       std::vector<uint32_t>& ids, std::vector<float>& dists, std::vector<uint32_t>& n) {
+  std::string e = sync_device(ix);
+  if (!e.empty()) return e;
+  if (size == 0) {
+    n.assign(nq, 0);
+    return "";
+  }
+  ids.resize((size_t)nq * size);
+  dists.resize((size_t)nq * size);
+  n.resize(nq);
+  // sc.radius stays FLT_MAX in ngt_linear_search_index_ (Capi.cpp:441-456)
+  if (ngt_amd_linear_search(ix->dev, queries, nq, (uint32_t)size, (double)FLT_MAX, ids.data(),
+                            dists.data(), n.data()))
+    return amd_err();
+  return "";
+}
+
+void fill_results(NGTObjectDistances results, const std::vector<uint32_t>& ids,
+                  const std::vector<float>& dists, uint32_t n) {
+  Results* r = static_cast<Results*>(results);
+  r->clear();
+  for (uint32_t i = 0; i < n; i++) r->push_back(NGTObjectDistance{ids[i], dists[i]});
+}
+
+HostProperty* prop_of(NGTProperty p) { return static_cast<HostProperty*>(p); }
+
+std::string create_empty(CapiIndex* ix, const HostProperty& prop) {
+  ix->host = HostIndex();
+  ix->host.prop = prop;
+  if (prop.dimension <= 0) return "dimension is not specified";
+  ix->host.init_layout();
+  ix->host.nrows = 1;  // dummy slot 0 (ObjectRepository.h:37-40)
+  ix->host.rows.assign(ix->host.row_bytes, 0);
+  ix->host.valid.assign(1, 0);
+  ix->host.edge_off.assign(2, 0);
+  ix->device_stale = true;
+  return "";
+}
+
+// Append one object to the host mirror, converting like
+// ObjectRepository::allocateObject (ObjectRepository.h:222-253).  The
+// normalization of stored objects for normalized metrics is part of index
+// construction and is rejected here.
+template <typename T>
+std::string append_object(CapiIndex* ix, const T* obj, uint32_t dim, uint32_t& id) {
+  HostIndex& h = ix->host;
+  if ((int32_t)dim != h.prop.dimension) return "the specified dimension is invalid";
+  int m = h.prop.distance_type;
+  if (m == 5 || m == 6 || m == 9) return "inserting into normalized-distance indexes is not implemented";
+  id = (uint32_t)h.nrows;
+  h.rows.resize((h.nrows + 1) * h.row_bytes, 0);
+  uint8_t* row = h.rows.data() + h.nrows * h.row_bytes;
+  if (h.prop.object_type == 2) {
+    float* f = reinterpret_cast<float*>(row);
+    for (uint32_t i = 0; i < dim; i++) f[i] = static_cast<float>(obj[i]);
+  } else {
+    for (uint32_t i = 0; i < dim; i++) row[i] = static_cast<uint8_t>(obj[i]);
+  }
+  h.valid.push_back(1);
+  h.nrows++;
+  h.edge_off.push_back(h.edge_off.back());
+  ix->device_stale = true;
+  return "";
+}
+
+const char* kNotImplemented =
+    "not implemented in the MI355X build yet (index construction / graph maintenance, SURVEY.md 8(f))";
+
+}  // namespace
+
+extern "C" {
+
+NGTIndex ngt_open_index(const char* index_path, NGTError error) {
+  try {
+    CapiIndex* ix = new CapiIndex();
+    // the device copy is built lazily on the first search (sync_device)
+    std::string e = ngt_amd::load_index(index_path, ix->host);
+    if (!e.empty()) {
+      delete ix;
+      set_error(error, __FUNCTION__, e);
+      return NULL;
+    }
+    return static_cast<NGTIndex>(ix);
+  } catch (std::exception& err) {
+    set_error(error, __FUNCTION__, err.what());
+    return NULL;
+  }
+}
+
+NGTIndex ngt_create_graph_and_tree(const char* database, NGTProperty prop, NGTError error) {
+  if (database == NULL || prop == NULL) {
+    param_error(error, __FUNCTION__, "database or prop is null");
+    return NULL;
+  }
+  CapiIndex* ix = new CapiIndex();
+  std::string e = create_empty(ix, *prop_of(prop));
+  if (e.empty()) {
+    mkdir(database, 0755);
+    e = ngt_amd::save_index(database, ix->host);
+  }
+  if (!e.empty()) {
+    delete ix;
+    set_error(error, __FUNCTION__, e);
+    return NULL;
+  }
+  return static_cast<NGTIndex>(ix);
+}
+
+NGTIndex ngt_create_graph_and_tree_in_memory(NGTProperty prop, NGTError error) {
+  if (prop == NULL) {
+    param_error(error, __FUNCTION__, "prop is null");
+    return NULL;
+  }
+  CapiIndex* ix = new CapiIndex();
+  std::string e = create_empty(ix, *prop_of(prop));
+  if (!e.empty()) {
+    delete ix;
+    set_error(error, __FUNCTION__, e);
+    return NULL;
+  }
+  return static_cast<NGTIndex>(ix);
+}
+
+NGTProperty ngt_create_property(NGTError error) {
+  try {
+    HostProperty* p = new HostProperty();
+    p->set_defaults();
+    return static_cast<NGTProperty>(p);
+  } catch (std::exception& err) {
+    set_error(error, __FUNCTION__, err.what());
+    return NULL;
+  }
+}
+
+bool ngt_save_index(const NGTIndex index, const char* database, NGTError error) {
+  if (index == NULL || database == NULL) {
+    param_error(error, __FUNCTION__, "index or database is null");
+    return false;
+  }
+  mkdir(database, 0755);
+  std::string e = ngt_amd::save_index(database, static_cast<CapiIndex*>(index)->host);
+  if (!e.empty()) {
+    set_error(error, __FUNCTION__, e);
+    return false;
+  }
+  return true;
+}
+
+bool ngt_get_property(NGTIndex index, NGTProperty prop, NGTError error) {
+  if (index == NULL || prop == NULL) {
+    std::stringstream ss;
+    ss << "index = " << index << " prop = " << prop;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  *prop_of(prop) = static_cast<CapiIndex*>(index)->host.prop;
+  return true;
+}
+
+#define PROP_GUARD(RET)                                        \
+  if (prop == NULL) {                                          \
+    std::stringstream ss;                                      \
+    ss << "prop = " << prop;                                   \
+    param_error(error, __FUNCTION__, ss.str());                \
+    return RET;                                                \
+  }
+
+int32_t ngt_get_property_dimension(NGTProperty prop, NGTError error) {
+  PROP_GUARD(-1);
+  return prop_of(prop)->dimension;
+}
+bool ngt_set_property_dimension(NGTProperty prop, int32_t value, NGTError error) {
+  PROP_GUARD(false);
+  prop_of(prop)->dimension = value;
+  return true;
+}
+bool ngt_set_property_edge_size_for_creation(NGTProperty prop, int16_t value, NGTError error) {
+  PROP_GUARD(false);
+  prop_of(prop)->edge_size_for_creation = value;
+  return true;
+}
+bool ngt_set_property_edge_size_for_search(NGTProperty prop, int16_t value, NGTError error) {
+  PROP_GUARD(false);
+  prop_of(prop)->edge_size_for_search = value;
+  return true;
+}
+int32_t ngt_get_property_object_type(NGTProperty prop, NGTError error) {
+  PROP_GUARD(-1);
+  return prop_of(prop)->object_type;
+}
+bool ngt_is_property_object_type_float(int32_t object_type) { return object_type == 2; }
+bool ngt_is_property_object_type_integer(int32_t object_type) { return object_type == 1; }
+bool ngt_set_property_object_type_float(NGTProperty prop, NGTError error) {
+  PROP_GUARD(false);
+  prop_of(prop)->object_type = 2;
+  return true;
+}
+bool ngt_set_property_object_type_integer(NGTProperty prop, NGTError error) {
+  PROP_GUARD(false);
+  prop_of(prop)->object_type = 1;
+  return true;
+}
+#define SET_DIST(FN, VAL)                       \
+  bool FN(NGTProperty prop, NGTError error) {   \
+    PROP_GUARD(false);                          \
+    prop_of(prop)->distance_type = VAL;         \
+    return true;                                \
+  }
+SET_DIST(ngt_set_property_distance_type_l1, 0)
+SET_DIST(ngt_set_property_distance_type_l2, 1)
+SET_DIST(ngt_set_property_distance_type_angle, 3)
+SET_DIST(ngt_set_property_distance_type_hamming, 2)
+SET_DIST(ngt_set_property_distance_type_jaccard, 7)
+SET_DIST(ngt_set_property_distance_type_cosine, 4)
+SET_DIST(ngt_set_property_distance_type_normalized_angle, 5)
+SET_DIST(ngt_set_property_distance_type_normalized_cosine, 6)
+#undef SET_DIST
+
+int16_t ngt_get_property_edge_size_for_creation(NGTProperty prop, NGTError error) {
+  PROP_GUARD(-1);
+  return (int16_t)prop_of(prop)->edge_size_for_creation;
+}
+int16_t ngt_get_property_edge_size_for_search(NGTProperty prop, NGTError error) {
+  PROP_GUARD(-1);
+  return (int16_t)prop_of(prop)->edge_size_for_search;
+}
+int32_t ngt_get_property_distance_type(NGTProperty prop, NGTError error) {
+  PROP_GUARD(-1);
+  return prop_of(prop)->distance_type;
+}
+
+NGTObjectDistances ngt_create_empty_results(NGTError error) {
+  try {
+    return static_cast<NGTObjectDistances>(new Results());
+  } catch (std::exception& err) {
+    set_error(error, __FUNCTION__, err.what());
+    return NULL;
+  }
+}
+
+static bool search_one(const char* func, NGTIndex index, const float* q, size_t size, float epsilon,
+                       float radius, int64_t edge_size, NGTObjectDistances results, NGTError error) {
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  std::vector<uint32_t> ids, n;
+  std::vector<float> dists;
+  if (radius < 0.0f) radius = FLT_MAX;  // Capi.cpp:357-359
+  std::string e = run_search(ix, q, 1, size, epsilon, radius, edge_size,
+                             use_tree(ix) ? NGT_AMD_SEED_TREE : NGT_AMD_SEED_RANDOM, ids, dists, n);
+  if (!e.empty()) {
+    set_error(error, func, e);
+    return false;
+  }
+  fill_results(results, ids, dists, n.empty() ? 0 : n[0]);
+  return true;
+}
+
+bool ngt_search_index(NGTIndex index, double* query, int32_t query_dim, size_t size, float epsilon,
+                      float radius, NGTObjectDistances results, NGTError error) {
+  if (index == NULL || query == NULL || results == NULL || query_dim <= 0) {
+    std::stringstream ss;
+    ss << "index = " << index << " query = " << query << " results = " << results << " query_dim = " << query_dim;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  std::vector<float> q(query, query + query_dim);
+  if (query_dim != static_cast<CapiIndex*>(index)->host.prop.dimension) {
+    set_error(error, __FUNCTION__, "the specified dimension is invalid");
+    return false;
+  }
+  return search_one(__FUNCTION__, index, q.data(), size, epsilon, radius, -1, results, error);
+}
+
+bool ngt_search_index_as_float(NGTIndex index, float* query, int32_t query_dim, size_t size, float epsilon,
+                               float radius, NGTObjectDistances results, NGTError error) {
+  if (index == NULL || query == NULL || results == NULL || query_dim <= 0) {
+    std::stringstream ss;
+    ss << "index = " << index << " query = " << query << " results = " << results << " query_dim = " << query_dim;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  if (query_dim != static_cast<CapiIndex*>(index)->host.prop.dimension) {
+    set_error(error, __FUNCTION__, "the specified dimension is invalid");
+    return false;
+  }
+  return search_one(__FUNCTION__, index, query, size, epsilon, radius, -1, results, error);
+}
+
+bool ngt_search_index_with_query(NGTIndex index, NGTQuery query, NGTObjectDistances results, NGTError error) {
+  if (index == NULL || query.query == NULL || results == NULL) {
+    std::stringstream ss;
+    ss << "index = " << index << " query = " << query.query << " results = " << results;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  return search_one(__FUNCTION__, index, query.query, query.size, query.epsilon, query.radius,
+                    (int64_t)(int)query.edge_size, results, error);
+}
+
+static bool linear_one(const char* func, NGTIndex index, const float* q, size_t size,
+                       NGTObjectDistances results, NGTError error) {
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  std::vector<uint32_t> ids, n;
+  std::vector<float> dists;
+  std::string e = run_linear(ix, q, 1, size, ids, dists, n);
+  if (!e.empty()) {
+    set_error(error, func, e);
+    return false;
+  }
+  fill_results(results, ids, dists, n.empty() ? 0 : n[0]);
+  return true;
+}
+
+bool ngt_linear_search_index(NGTIndex index, double* query, int32_t query_dim, size_t size,
+                             NGTObjectDistances results, NGTError error) {
+  if (index == NULL || query == NULL || results == NULL || query_dim <= 0) {
+    std::stringstream ss;
+    ss << "index = " << index << " query = " << query << " results = " << results << " query_dim = " << query_dim;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  std::vector<float> q(query, query + query_dim);
+  return linear_one(__FUNCTION__, index, q.data(), size, results, error);
+}
+
+bool ngt_linear_search_index_as_float(NGTIndex index, float* query, int32_t query_dim, size_t size,
+                                      NGTObjectDistances results, NGTError error) {
+  if (index == NULL || query == NULL || results == NULL || query_dim <= 0) {
+    std::stringstream ss;
+    ss << "index = " << index << " query = " << query << " results = " << results << " query_dim = " << query_dim;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  return linear_one(__FUNCTION__, index, query, size, results, error);
+}
+
+bool ngt_linear_search_index_with_query(NGTIndex index, NGTQuery query, NGTObjectDistances results,
+                                        NGTError error) {
+  if (index == NULL || query.query == NULL || results == NULL) {
+    std::stringstream ss;
+    ss << "index = " << index << " query = " << query.query << " results = " << results;
+    param_error(error, __FUNCTION__, ss.str());
+    return false;
+  }
+  return linear_one(__FUNCTION__, index, query.query, query.size, results, error);
+}
+
+int32_t ngt_get_size(NGTObjectDistances results, NGTError error) {
+  if (results == NULL) {
+    param_error(error, __FUNCTION__, "results = 0");
+    return -1;
+  }
+  return (int32_t) static_cast<Results*>(results)->size();
+}
+
+uint32_t ngt_get_result_size(NGTObjectDistances results, NGTError error) {
+  if (results == NULL) {
+    param_error(error, __FUNCTION__, "results = 0");
+    return 0;
+  }
+  return (uint32_t) static_cast<Results*>(results)->size();
+}
+
+NGTObjectDistance ngt_get_result(const NGTObjectDistances results, const uint32_t i, NGTError error) {
+  Results* r = static_cast<Results*>(results);
+  if (r == NULL || i >= r->size()) {
+    set_error(error, __FUNCTION__, "index out of range");
+    NGTObjectDistance err_val = {0, 0.0f};
+    return err_val;
+  }
+  return (*r)[i];
+}
+
+ObjectID ngt_insert_index(NGTIndex index, double* obj, uint32_t obj_dim, NGTError error) {
+  if (index == NULL || obj == NULL || obj_dim == 0) {
+    param_error(error, __FUNCTION__, "index or obj is null");
+    return 0;
+  }
+  uint32_t id = 0;
+  std::string e = append_object(static_cast<CapiIndex*>(index), obj, obj_dim, id);
+  if (!e.empty()) {
+    set_error(error, __FUNCTION__, e);
+    return 0;
+  }
+  return id;
+}
+ObjectID ngt_append_index(NGTIndex index, double* obj, uint32_t obj_dim, NGTError error) {
+  return ngt_insert_index(index, obj, obj_dim, error);
+}
+ObjectID ngt_insert_index_as_float(NGTIndex index, float* obj, uint32_t obj_dim, NGTError error) {
+  if (index == NULL || obj == NULL || obj_dim == 0) {
+    param_error(error, __FUNCTION__, "index or obj is null");
+    return 0;
+  }
+  uint32_t id = 0;
+  std::string e = append_object(static_cast<CapiIndex*>(index), obj, obj_dim, id);
+  if (!e.empty()) {
+    set_error(error, __FUNCTION__, e);
+    return 0;
+  }
+  return id;
+}
+ObjectID ngt_append_index_as_float(NGTIndex index, float* obj, uint32_t obj_dim, NGTError error) {
+  return ngt_insert_index_as_float(index, obj, obj_dim, error);
+}
+bool ngt_batch_append_index(NGTIndex index, float* obj, uint32_t data_count, NGTError error) {
+  if (index == NULL || obj == NULL) {
+    param_error(error, __FUNCTION__, "index or obj is null");
+    return false;
+  }
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  uint32_t dim = (uint32_t)ix->host.prop.dimension, id;
+  for (uint32_t i = 0; i < data_count; i++) {
+    std::string e = append_object(ix, obj + (size_t)i * dim, dim, id);
+    if (!e.empty()) {
+      set_error(error, __FUNCTION__, e);
+      return false;
+    }
+  }
+  return true;
+}
+bool ngt_batch_insert_index(NGTIndex index, float* obj, uint32_t num_obj, uint32_t* obj_ids, NGTError error) {
+  if (!ngt_batch_append_index(index, obj, num_obj, error)) return false;
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  if (obj_ids)
+    for (uint32_t i = 0; i < num_obj; i++) obj_ids[i] = (uint32_t)(ix->host.nrows - num_obj + i);
+  return ngt_create_index(index, 0, error);
+}
+bool ngt_create_index(NGTIndex index, uint32_t pool_size, NGTError error) {
+  (void)pool_size;
+  if (index == NULL) {
+    param_error(error, __FUNCTION__, "index = 0");
+    return false;
+  }
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+bool ngt_remove_index(NGTIndex index, ObjectID id, NGTError error) {
+  (void)id;
+  if (index == NULL) {
+    param_error(error, __FUNCTION__, "index = 0");
+    return false;
+  }
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+
+NGTObjectSpace ngt_get_object_space(NGTIndex index, NGTError error) {
+  if (index == NULL) {
+    param_error(error, __FUNCTION__, "index = 0");
+    return NULL;
+  }
+  return static_cast<NGTObjectSpace>(index);
+}
+
+float* ngt_get_object_as_float(NGTObjectSpace object_space, ObjectID id, NGTError error) {
+  CapiIndex* ix = static_cast<CapiIndex*>(object_space);
+  if (ix == NULL) {
+    param_error(error, __FUNCTION__, "object_space = 0");
+    return NULL;
+  }
+  HostIndex& h = ix->host;
+  if (id == 0 || id >= h.nrows || !h.valid[id]) {
+    std::stringstream ss;
+    ss << "NGT::ObjectSpaceRepository: The specified ID is out of the range. The object ID should be greater than zero. "
+       << id << ":" << h.nrows << ".";
+    set_error(error, __FUNCTION__, ss.str());
+    return NULL;
+  }
+  if (h.prop.object_type != 2) {
+    set_error(error, __FUNCTION__, "the object type is not float");
+    return NULL;
+  }
+  return reinterpret_cast<float*>(h.rows.data() + (size_t)id * h.row_bytes);
+}
+
+uint8_t* ngt_get_object_as_integer(NGTObjectSpace object_space, ObjectID id, NGTError error) {
+  CapiIndex* ix = static_cast<CapiIndex*>(object_space);
+  if (ix == NULL) {
+    param_error(error, __FUNCTION__, "object_space = 0");
+    return NULL;
+  }
+  HostIndex& h = ix->host;
+  if (id == 0 || id >= h.nrows || !h.valid[id]) {
+    set_error(error, __FUNCTION__, "the specified ID is out of the range");
+    return NULL;
+  }
+  if (h.prop.object_type != 1) {
+    set_error(error, __FUNCTION__, "the object type is not integer");
+    return NULL;
+  }
+  return h.rows.data() + (size_t)id * h.row_bytes;
+}
+
+void ngt_destroy_results(NGTObjectDistances results) { delete static_cast<Results*>(results); }
+void ngt_destroy_property(NGTProperty prop) { delete prop_of(prop); }
+void ngt_close_index(NGTIndex index) { delete static_cast<CapiIndex*>(index); }
+
+NGTError ngt_create_error_object() {
+  try {
+    return static_cast<NGTError>(new std::string());
+  } catch (std::exception& err) {
+    std::cerr << "Capi : " << __FUNCTION__ << "() : Error: " << err.what();
+    return NULL;
+  }
+}
+const char* ngt_get_error_string(const NGTError error) {
+  return static_cast<std::string*>(error)->c_str();
+}
+void ngt_clear_error_string(NGTError error) { *static_cast<std::string*>(error) = ""; }
+void ngt_destroy_error_object(NGTError error) { delete static_cast<std::string*>(error); }
+
+NGTOptimizer ngt_create_optimizer(bool, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return NULL;
+}
+bool ngt_optimizer_adjust_search_coefficients(NGTOptimizer, const char*, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+bool ngt_optimizer_execute(NGTOptimizer, const char*, const char*, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+bool ngt_optimizer_set(NGTOptimizer, int, int, int, float, float, float, float, double, double,
+                       NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+bool ngt_optimizer_set_minimum(NGTOptimizer, int, int, int, int, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+bool ngt_optimizer_set_extension(NGTOptimizer, float, float, float, float, double, double, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+bool ngt_optimizer_set_processing_modes(NGTOptimizer, bool, bool, bool, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+void ngt_destroy_optimizer(NGTOptimizer) {}
+bool ngt_refine_anng(NGTIndex, float, float, int, int, size_t, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+
+bool ngt_get_edges(NGTIndex index, ObjectID id, NGTObjectDistances edges, NGTError error) {
+  if (index == NULL || edges == NULL) {
+    param_error(error, __FUNCTION__, "index or edges is null");
+    return false;
+  }
+  HostIndex& h = static_cast<CapiIndex*>(index)->host;
+  if (id == 0 || id >= h.nrows) {
+    set_error(error, __FUNCTION__, "the specified ID is out of the range");
+    return false;
+  }
+  Results* r = static_cast<Results*>(edges);
+  r->clear();
+  for (uint64_t j = h.edge_off[id]; j < h.edge_off[id + 1]; j++)
+    r->push_back(NGTObjectDistance{h.edges[j], j < h.edge_dists.size() ? h.edge_dists[j] : 0.f});
+  return true;
+}
+
+uint32_t ngt_get_object_repository_size(NGTIndex index, NGTError error) {
+  if (index == NULL) {
+    param_error(error, __FUNCTION__, "index = 0");
+    return 0;
+  }
+  return (uint32_t) static_cast<CapiIndex*>(index)->host.nrows;
+}
+
+NGTAnngEdgeOptimizationParameter ngt_get_anng_edge_optimization_parameter() {
+  NGTAnngEdgeOptimizationParameter p;
+  p.no_of_queries = 200;
+  p.no_of_results = 50;
+  p.no_of_threads = 16;
+  p.target_accuracy = 0.9f;
+  p.target_no_of_objects = 0;
+  p.no_of_sample_objects = 100000;
+  p.max_of_no_of_edges = 100;
+  p.log = false;
+  return p;
+}
+bool ngt_optimize_number_of_edges(const char*, NGTAnngEdgeOptimizationParameter, NGTError error) {
+  set_error(error, __FUNCTION__, kNotImplemented);
+  return false;
+}
+
+// ---- extensions --------------------------------------------------------------
+static bool batch_search(const char* func, NGTIndex index, const float* queries, uint32_t nq, int32_t dim,
+                         size_t size, float epsilon, float radius, int64_t edge_size, int seed_mode,
+                         uint32_t* ids, float* dists, uint32_t* n, NGTError error) {
+  if (index == NULL || queries == NULL || ids == NULL || dists == NULL || n == NULL) {
+    param_error(error, func, "null argument");
+    return false;
+  }
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  if (dim != ix->host.prop.dimension) {
+    set_error(error, func, "the specified dimension is invalid");
+    return false;
+  }
+  std::vector<uint32_t> vi, vn;
+  std::vector<float> vd;
+  std::string e = run_search(ix, queries, nq, size, epsilon, radius, edge_size, seed_mode, vi, vd, vn);
+  if (!e.empty()) {
+    set_error(error, func, e);
+    return false;
+  }
+  memcpy(ids, vi.data(), vi.size() * sizeof(uint32_t));
+  memcpy(dists, vd.data(), vd.size() * sizeof(float));
+  memcpy(n, vn.data(), vn.size() * sizeof(uint32_t));
+  return true;
+}
+
+bool ngt_batch_search_index(NGTIndex index, const float* queries, uint32_t nq, int32_t dim, size_t size,
+                            float epsilon, float radius, int64_t edge_size, uint32_t* ids, float* dists,
+                            uint32_t* n, NGTError error) {
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  int mode = ix && use_tree(ix) ? NGT_AMD_SEED_TREE : NGT_AMD_SEED_RANDOM;
+  return batch_search(__FUNCTION__, index, queries, nq, dim, size, epsilon, radius, edge_size, mode, ids,
+                      dists, n, error);
+}
+
+bool ngt_batch_search_index_using_only_graph(NGTIndex index, const float* queries, uint32_t nq, int32_t dim,
+                                             size_t size, float epsilon, float radius, int64_t edge_size,
+                                             uint32_t* ids, float* dists, uint32_t* n, NGTError error) {
+  return batch_search(__FUNCTION__, index, queries, nq, dim, size, epsilon, radius, edge_size,
+                      NGT_AMD_SEED_RANDOM, ids, dists, n, error);
+}
+
+bool ngt_batch_linear_search_index(NGTIndex index, const float* queries, uint32_t nq, int32_t dim, size_t size,
+                                   uint32_t* ids, float* dists, uint32_t* n, NGTError error) {
+  if (index == NULL || queries == NULL || ids == NULL || dists == NULL || n == NULL) {
+    param_error(error, __FUNCTION__, "null argument");
+    return false;
+  }
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  if (dim != ix->host.prop.dimension) {
+    set_error(error, __FUNCTION__, "the specified dimension is invalid");
+    return false;
+  }
+  std::vector<uint32_t> vi, vn;
+  std::vector<float> vd;
+  std::string e = run_linear(ix, queries, nq, size, vi, vd, vn);
+  if (!e.empty()) {
+    set_error(error, __FUNCTION__, e);
+    return false;
+  }
+  memcpy(ids, vi.data(), vi.size() * sizeof(uint32_t));
+  memcpy(dists, vd.data(), vd.size() * sizeof(float));
+  memcpy(n, vn.data(), vn.size() * sizeof(uint32_t));
+  return true;
+}
+
+bool ngt_get_last_search_counters(NGTIndex index, uint64_t* counters3, NGTError error) {
+  if (index == NULL || counters3 == NULL) {
+    param_error(error, __FUNCTION__, "null argument");
+    return false;
+  }
+  memcpy(counters3, static_cast<CapiIndex*>(index)->last_counters, 3 * sizeof(uint64_t));
+  return true;
+}
+
+}  // extern "C"

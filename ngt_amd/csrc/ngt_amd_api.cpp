@@ -1,0 +1,605 @@
+// ngt_amd_api.cpp -- host side of the C ABI declared in include/ngt_amd.h.
+//
+// Owns the HBM layout of an index (padded row-major object slab, CSR
+// adjacency, flattened DVP tree, per-slot search scratch) and enqueues the
+// gfx950 kernels of search_kernels.hip / prep_kernels.hip.  There is no CPU
+// compute path: every distance is evaluated on the device.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <climits>
+#include <cfloat>
+#include <string>
+#include <vector>
+
+#include "../../include/ngt_amd.h"
+#include "ngt_kernels.h"
+#include "prep_kernels.h"
+
+using namespace ngt_amd;
+
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+
+#define HIP_OK(expr)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  bool owned = true;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p && owned) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    owned = true;
+  }
+  hipError_t alloc(size_t count) {
+    if (p && owned && n >= count) return hipSuccess;
+    release();
+    n = count;
+    return hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+  }
+  hipError_t upload(const T* h, size_t count) {
+    hipError_t e = alloc(count);
+    if (e != hipSuccess) return e;
+    if (count) e = hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+  }
+};
+
+struct ngt_amd_index {
+  int device = 0;
+  int metric = 1;
+  int otype = 2;
+  uint32_t dim = 0;
+  uint32_t dp = 0;
+  uint32_t esize = 4;
+  uint64_t row_bytes = 0;
+  uint64_t nrows = 0;
+  DevBuf<uint8_t> rows, valid;
+  std::vector<uint8_t> h_valid;
+  std::vector<uint64_t> h_degree_nonzero;  // for isEmpty in getRandomSeeds
+  DevBuf<uint64_t> edge_off;
+  DevBuf<uint32_t> edges;
+  uint64_t nedges = 0;
+  bool has_graph = false;
+  std::vector<uint8_t> h_graph_empty;
+  // tree
+  bool has_tree = false;
+  DevBuf<uint8_t> in_pivot;
+  DevBuf<uint32_t> in_child, leaf_ids;
+  DevBuf<float> in_border;
+  DevBuf<uint64_t> leaf_off;
+  uint32_t children = 5, root = 0;
+  // property
+  int32_t edge_size_for_search = 0;
+  int32_t dyn_base = 30, dyn_rate = 20;
+  int32_t seed_size = 10, seed_type = 0;
+  // scratch
+  DevBuf<uint32_t> bitmap, work, seeds, seed_count;
+  DevBuf<uint64_t> spill, seed_off;
+  DevBuf<int> error;
+  uint32_t slots = 0;
+  uint64_t bitmap_words = 0;
+  uint32_t spill_cap = 1u << 16;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0.f;
+  int cu_count = 256;
+  size_t lds_per_cu = 160 * 1024;
+};
+
+extern "C" const char* ngt_amd_last_error(void) { return g_err.c_str(); }
+
+extern "C" int ngt_amd_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+static bool valid_metric(int m) {
+  return (m >= 0 && m <= 9) || m == 100 || m == 101;
+}
+
+extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distance_type,
+                                    int object_type, uint32_t dimension) {
+  if (!out) return fail("ngt_amd_index_create: out is null");
+  *out = nullptr;
+  if (!valid_metric(distance_type)) return fail("ngt_amd_index_create: invalid distance type %d", distance_type);
+  if (object_type != 1 && object_type != 2) return fail("ngt_amd_index_create: invalid object type %d", object_type);
+  if (dimension == 0) return fail("ngt_amd_index_create: dimension is 0");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail("ngt_amd_index_create: no HIP device available (the MI355X path has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail("ngt_amd_index_create: device %d out of range", device);
+  HIP_OK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, device));
+  auto* ix = new ngt_amd_index();
+  ix->device = device;
+  ix->metric = distance_type;
+  ix->otype = object_type;
+  ix->dim = dimension;
+  // SparseJaccard keeps dimension+1 slots (Index.cpp:488-490 is the caller's job)
+  ix->dp = ((dimension - 1) / 16 + 1) * 16;
+  ix->esize = object_type == 2 ? 4 : 1;
+  ix->row_bytes = (uint64_t)ix->dp * ix->esize;
+  ix->cu_count = prop.multiProcessorCount;
+  ix->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
+  if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ix->ev0) != hipSuccess || hipEventCreate(&ix->ev1) != hipSuccess) {
+    delete ix;
+    return fail("ngt_amd_index_create: stream/event creation failed");
+  }
+  if (ix->error.alloc(1) != hipSuccess || ix->work.alloc(4) != hipSuccess) {
+    delete ix;
+    return fail("ngt_amd_index_create: allocation failed");
+  }
+  (void)hipMemset(ix->error.p, 0, sizeof(int));
+  *out = ix;
+  return 0;
+}
+
+extern "C" void ngt_amd_index_destroy(ngt_amd_index* ix) {
+  if (!ix) return;
+  (void)hipSetDevice(ix->device);
+  if (ix->stream) (void)hipStreamSynchronize(ix->stream);
+  if (ix->ev0) (void)hipEventDestroy(ix->ev0);
+  if (ix->ev1) (void)hipEventDestroy(ix->ev1);
+  if (ix->stream) (void)hipStreamDestroy(ix->stream);
+  delete ix;
+}
+
+extern "C" uint32_t ngt_amd_index_padded_dimension(const ngt_amd_index* ix) {
+  return ix ? ix->dp : 0;
+}
+
+extern "C" int ngt_amd_index_set_objects(ngt_amd_index* ix, const void* rows, uint64_t nrows,
+                                         const uint8_t* valid) {
+  if (!ix || !rows || nrows == 0) return fail("ngt_amd_index_set_objects: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  HIP_OK(ix->rows.upload(static_cast<const uint8_t*>(rows), nrows * ix->row_bytes));
+  ix->nrows = nrows;
+  ix->h_valid.assign(nrows, 1);
+  ix->h_valid[0] = 0;
+  if (valid) ix->h_valid.assign(valid, valid + nrows);
+  HIP_OK(ix->valid.upload(ix->h_valid.data(), nrows));
+  return 0;
+}
+
+extern "C" int ngt_amd_index_set_objects_device(ngt_amd_index* ix, const void* d_rows, uint64_t nrows) {
+  if (!ix || !d_rows || nrows == 0) return fail("ngt_amd_index_set_objects_device: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  ix->rows.release();
+  ix->rows.p = (uint8_t*)d_rows;
+  ix->rows.n = nrows * ix->row_bytes;
+  ix->rows.owned = false;
+  ix->nrows = nrows;
+  ix->h_valid.assign(nrows, 1);
+  ix->h_valid[0] = 0;
+  HIP_OK(ix->valid.upload(ix->h_valid.data(), nrows));
+  return 0;
+}
+
+static void note_graph_empty(ngt_amd_index* ix, const uint64_t* offsets, uint64_t nrows) {
+  ix->h_graph_empty.assign(nrows, 1);
+  for (uint64_t i = 0; i < nrows; i++) ix->h_graph_empty[i] = offsets[i + 1] == offsets[i];
+}
+
+extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offsets,
+                                       const uint32_t* edges, uint64_t nedges) {
+  if (!ix || !offsets || (!edges && nedges)) return fail("ngt_amd_index_set_graph: bad arguments");
+  if (ix->nrows == 0) return fail("ngt_amd_index_set_graph: set the objects first");
+  if (offsets[ix->nrows] != nedges) return fail("ngt_amd_index_set_graph: offsets[nrows] != nedges");
+  for (uint64_t i = 0; i < nedges; i++)
+    if (edges[i] == 0 || edges[i] >= ix->nrows)
+      return fail("ngt_amd_index_set_graph: edge %llu -> %u out of range", (unsigned long long)i, edges[i]);
+  HIP_OK(hipSetDevice(ix->device));
+  HIP_OK(ix->edge_off.upload(offsets, ix->nrows + 1));
+  HIP_OK(ix->edges.upload(edges, nedges));
+  ix->nedges = nedges;
+  ix->has_graph = true;
+  note_graph_empty(ix, offsets, ix->nrows);
+  return 0;
+}
+
+extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t* d_offsets,
+                                              const uint32_t* d_edges, uint64_t nedges) {
+  if (!ix || !d_offsets) return fail("ngt_amd_index_set_graph_device: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  ix->edge_off.release();
+  ix->edges.release();
+  ix->edge_off.p = const_cast<uint64_t*>(d_offsets);
+  ix->edge_off.owned = false;
+  ix->edges.p = const_cast<uint32_t*>(d_edges);
+  ix->edges.owned = false;
+  ix->nedges = nedges;
+  ix->has_graph = true;
+  std::vector<uint64_t> h(ix->nrows + 1);
+  HIP_OK(hipMemcpy(h.data(), d_offsets, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  note_graph_empty(ix, h.data(), ix->nrows);
+  return 0;
+}
+
+extern "C" int ngt_amd_index_set_tree(ngt_amd_index* ix, const void* in_pivot, uint32_t n_internal,
+                                      const uint32_t* in_child, const float* in_border,
+                                      uint32_t children, uint32_t root, const uint64_t* leaf_off,
+                                      uint32_t n_leaf, const uint32_t* leaf_ids, uint64_t n_leaf_ids) {
+  if (!ix || children < 2 || !leaf_off) return fail("ngt_amd_index_set_tree: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  HIP_OK(ix->in_pivot.upload(static_cast<const uint8_t*>(in_pivot), (size_t)n_internal * ix->row_bytes));
+  HIP_OK(ix->in_child.upload(in_child, (size_t)n_internal * children));
+  HIP_OK(ix->in_border.upload(in_border, (size_t)n_internal * (children - 1)));
+  HIP_OK(ix->leaf_off.upload(leaf_off, (size_t)n_leaf + 1));
+  HIP_OK(ix->leaf_ids.upload(leaf_ids, n_leaf_ids));
+  ix->children = children;
+  ix->root = root;
+  ix->has_tree = true;
+  return 0;
+}
+
+extern "C" int ngt_amd_index_set_search_property(ngt_amd_index* ix, int32_t edge_size_for_search,
+                                                 int32_t dynamic_edge_size_base,
+                                                 int32_t dynamic_edge_size_rate, int32_t seed_size,
+                                                 int32_t seed_type) {
+  if (!ix) return fail("ngt_amd_index_set_search_property: null index");
+  ix->edge_size_for_search = edge_size_for_search;
+  ix->dyn_base = dynamic_edge_size_base;
+  ix->dyn_rate = dynamic_edge_size_rate;
+  ix->seed_size = seed_size;
+  ix->seed_type = seed_type;
+  return 0;
+}
+
+static float coef_of(float epsilon) {
+  // SearchContainer::setEpsilon (Common.h:2041); 0 => NGT_EXPLORATION_COEFFICIENT (Graph.cpp:403-405)
+  float c = (float)((double)epsilon + 1.0);
+  if (c == 0.0f) c = (float)1.1;
+  return c;
+}
+
+extern "C" uint64_t ngt_amd_resolve_edge_size(const ngt_amd_index* ix, int64_t edge_size, float epsilon) {
+  // NeighborhoodGraph::getEdgeSize (Graph.h:675-692)
+  int64_t esize = edge_size == -1 ? ix->edge_size_for_search : edge_size;
+  if (esize == 0) return INT_MAX;
+  if (esize > 0) return (uint64_t)esize;
+  if (esize == -2) {
+    float coef = coef_of(epsilon);
+    double add = pow(10, ((double)coef - 1.0) * (double)(float)ix->dyn_rate);
+    return add >= (double)INT_MAX ? (uint64_t)INT_MAX : (uint64_t)(ix->dyn_base + add);
+  }
+  return 0;  // invalid -> caller reports
+}
+
+static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a) {
+  size_t lds = search_lds_bytes(a, ix->otype);
+  if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
+  uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
+  if (per_cu > 16) per_cu = 16;
+  if (per_cu < 1) per_cu = 1;
+  uint32_t slots = per_cu * (uint32_t)ix->cu_count;
+  uint64_t words = ((ix->nrows + 31) / 32 + 3) & ~3ull;
+  if (slots != ix->slots || words != ix->bitmap_words || !ix->spill.p) {
+    HIP_OK(ix->bitmap.alloc((size_t)slots * words));
+    HIP_OK(hipMemset(ix->bitmap.p, 0, (size_t)slots * words * sizeof(uint32_t)));
+    HIP_OK(ix->spill.alloc((size_t)slots * ix->spill_cap));
+    ix->slots = slots;
+    ix->bitmap_words = words;
+  }
+  return 0;
+}
+
+static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const void* d_queries,
+                      uint64_t query_bytes, uint32_t nq, const uint32_t* d_seeds,
+                      const uint64_t* d_seed_off, uint32_t* d_ids, float* d_dists, uint32_t* d_n,
+                      uint64_t* d_counters, hipStream_t s) {
+  if (!ix->has_graph) return fail("search: the index has no graph");
+  if (prm->k == 0) return fail("search: k must be > 0");
+  uint64_t es = ngt_amd_resolve_edge_size(ix, prm->edge_size, prm->epsilon);
+  if (es == 0) return fail("search: invalid edge size %lld", (long long)prm->edge_size);
+
+  SearchArgs a{};
+  a.rows = ix->rows.p;
+  a.row_bytes = ix->row_bytes;
+  a.nrows = (uint32_t)ix->nrows;
+  a.dp = (int)ix->dp;
+  a.edge_off = ix->edge_off.p;
+  a.edges = ix->edges.p;
+  a.queries = static_cast<const uint8_t*>(d_queries);
+  a.query_bytes = query_bytes;
+  a.nq = nq;
+  a.k = prm->k;
+  a.coef = coef_of(prm->epsilon);
+  a.radius = prm->radius < 0.0f ? FLT_MAX : prm->radius;
+  a.edge_size = es;
+  // LDS capacities of the visited hash and the unchecked array; overridable
+  // (NGT_AMD_HT_LOG2 / NGT_AMD_CQ_CAP) so tests can force the exact HBM
+  // overflow paths.
+  a.ht_log2 = 12;
+  a.cq_cap = 1024;
+  if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
+  if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+  a.out_ids = d_ids;
+  a.out_dists = d_dists;
+  a.out_n = d_n;
+  a.counters = d_counters;
+  a.error = ix->error.p;
+
+  if (prm->seed_mode == NGT_AMD_SEED_TREE) {
+    if (!ix->has_tree) return fail("search: tree seeds requested but the index has no tree");
+    const uint32_t stride = 128;
+    HIP_OK(ix->seeds.alloc((size_t)nq * stride));
+    HIP_OK(ix->seed_count.alloc(nq));
+    TreeSeedArgs t{};
+    t.queries = a.queries;
+    t.query_bytes = query_bytes;
+    t.nq = nq;
+    t.dp = a.dp;
+    t.row_bytes = ix->row_bytes;
+    t.in_pivot = ix->in_pivot.p;
+    t.in_child = ix->in_child.p;
+    t.in_border = ix->in_border.p;
+    t.children = ix->children;
+    t.root = ix->root;
+    t.leaf_off = ix->leaf_off.p;
+    t.leaf_ids = ix->leaf_ids.p;
+    t.seed_size = (uint32_t)std::max(ix->seed_size, 0);
+    t.k = prm->k;
+    t.all_leaf_nodes = prm->all_leaf_nodes || ix->seed_type == 4;
+    t.seeds = ix->seeds.p;
+    t.seed_stride = stride;
+    t.seed_count = ix->seed_count.p;
+    HIP_OK(launch_tree_seeds(t, ix->metric, ix->otype, s));
+    a.seeds = ix->seeds.p;
+    a.seed_stride = stride;
+    a.seed_count = ix->seed_count.p;
+  } else {
+    if (!d_seeds || !d_seed_off) return fail("search: seed lists required for this seed mode");
+    a.seeds = d_seeds;
+    a.seed_off = d_seed_off;
+  }
+  if (ensure_scratch(ix, a)) return -1;
+  a.bitmap = ix->bitmap.p;
+  a.bitmap_words = ix->bitmap_words;
+  a.spill = ix->spill.p;
+  a.spill_cap = ix->spill_cap;
+  a.work = ix->work.p;
+  HIP_OK(hipMemsetAsync(ix->work.p, 0, sizeof(uint32_t), s));
+  uint32_t slots = std::min<uint32_t>(ix->slots, nq);
+  HIP_OK(hipEventRecord(ix->ev0, s));
+  HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
+  HIP_OK(hipEventRecord(ix->ev1, s));
+  return 0;
+}
+
+static std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off) {
+  // GraphIndex::getRandomSeeds (Index.h:775-801) over the process-wide rand()
+  // stream, one query after another as the reference's callers do.
+  std::vector<uint32_t> seeds;
+  off.assign(nq + 1, 0);
+  size_t repo = ix->nrows == 0 ? 0 : ix->nrows - 1;
+  size_t ss = std::min<size_t>(repo, (size_t)std::max(ix->seed_size, 0));
+  for (uint32_t q = 0; q < nq; q++) {
+    size_t start = seeds.size();
+    size_t empty = 0;
+    while (seeds.size() - start < ss) {
+      double random = ((double)rand() + 1.0) / ((double)RAND_MAX + 2.0);
+      size_t idx = (size_t)floor((double)repo * random) + 1;
+      if (ix->h_graph_empty[idx]) {
+        if (++empty > repo) break;
+        continue;
+      }
+      if (std::find(seeds.begin() + start, seeds.end(), (uint32_t)idx) != seeds.end()) continue;
+      seeds.push_back((uint32_t)idx);
+    }
+    off[q + 1] = seeds.size();
+  }
+  return seeds;
+}
+
+extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_params* prm,
+                                     const void* d_queries, uint64_t query_bytes, uint32_t nq,
+                                     const uint32_t* d_seeds, const uint64_t* d_seed_off,
+                                     uint32_t* d_ids, float* d_dists, uint32_t* d_n,
+                                     uint64_t* d_counters, void* stream) {
+  if (!ix || !prm || (!d_queries && nq)) return fail("ngt_amd_search_device: bad arguments");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+  if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
+    HIP_OK(ix->seed_off.upload(off.data(), off.size()));
+    HIP_OK(ix->seeds.upload(seeds.data(), seeds.size()));
+    return run_search(ix, prm, d_queries, query_bytes, nq, ix->seeds.p, ix->seed_off.p, d_ids,
+                      d_dists, d_n, d_counters, s);
+  }
+  return run_search(ix, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, d_ids, d_dists,
+                    d_n, d_counters, s);
+}
+
+extern "C" float ngt_amd_last_search_kernel_ms(const ngt_amd_index* ix) {
+  if (!ix) return 0.f;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, ix->ev0, ix->ev1) != hipSuccess) return -1.f;
+  return ms;
+}
+
+// Upload host float queries and prepare them on the device.
+static int upload_queries(ngt_amd_index* ix, const void* queries, uint32_t nq, DevBuf<float>& raw,
+                          DevBuf<uint8_t>& prep, hipStream_t s) {
+  // host queries are float [nq][dim] for every object type (Index::allocateObject
+  // converts them to the object type, ObjectRepository.h:222-253)
+  HIP_OK(raw.upload(static_cast<const float*>(queries), (size_t)nq * ix->dim));
+  HIP_OK(prep.alloc((size_t)nq * ix->row_bytes));
+  if (ngt_amd_prepare_queries_device(ix, raw.p, nq, prep.p, s)) return -1;
+  return 0;
+}
+
+extern "C" int ngt_amd_prepare_queries_device(ngt_amd_index* ix, const float* d_in, uint32_t nq,
+                                              void* d_out, void* stream) {
+  if (!ix || (!d_in && nq) || (!d_out && nq)) return fail("ngt_amd_prepare_queries_device: bad arguments");
+  if (nq == 0) return 0;
+  hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+  bool normalize = ix->metric == 5 || ix->metric == 6 || ix->metric == 9;
+  HIP_OK(launch_prepare_queries(d_in, ix->dim, nq, ix->dp, ix->otype, normalize, d_out, ix->error.p, s));
+  return 0;
+}
+
+extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const void* queries,
+                              uint32_t nq, const uint32_t* seeds, const uint64_t* seed_off,
+                              uint32_t* ids, float* dists, uint32_t* n, uint64_t* counters) {
+  if (!ix || !prm || (!queries && nq) || !ids || !dists || !n) return fail("ngt_amd_search: bad arguments");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = ix->stream;
+  DevBuf<float> raw;
+  DevBuf<uint8_t> q;
+  if (upload_queries(ix, queries, nq, raw, q, s)) return -1;
+  DevBuf<uint32_t> d_ids, d_n, d_seeds;
+  DevBuf<float> d_dists;
+  DevBuf<uint64_t> d_cnt, d_seed_off;
+  HIP_OK(d_ids.alloc((size_t)nq * prm->k));
+  HIP_OK(d_dists.alloc((size_t)nq * prm->k));
+  HIP_OK(d_n.alloc(nq));
+  if (counters) HIP_OK(d_cnt.alloc((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY));
+  const uint32_t* sp = nullptr;
+  const uint64_t* so = nullptr;
+  if (prm->seed_mode == NGT_AMD_SEED_GIVEN) {
+    if (!seeds || !seed_off) return fail("ngt_amd_search: NGT_AMD_SEED_GIVEN needs seeds and seed_off");
+    for (uint64_t i = 0; i < seed_off[nq]; i++)
+      if (seeds[i] == 0 || seeds[i] >= ix->nrows) return fail("ngt_amd_search: seed id %u out of range", seeds[i]);
+    HIP_OK(d_seeds.upload(seeds, seed_off[nq]));
+    HIP_OK(d_seed_off.upload(seed_off, (size_t)nq + 1));
+    sp = d_seeds.p;
+    so = d_seed_off.p;
+  }
+  if (ngt_amd_search_device(ix, prm, q.p, ix->row_bytes, nq, sp, so, d_ids.p, d_dists.p, d_n.p,
+                            counters ? d_cnt.p : nullptr, s))
+    return -1;
+  HIP_OK(hipMemcpyAsync(ids, d_ids.p, (size_t)nq * prm->k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(dists, d_dists.p, (size_t)nq * prm->k * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(n, d_n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (counters)
+    HIP_OK(hipMemcpyAsync(counters, d_cnt.p, (size_t)nq * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
+                          hipMemcpyDeviceToHost, s));
+  int herr = 0;
+  HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  if (herr) {
+    (void)hipMemset(ix->error.p, 0, sizeof(int));
+    return fail("ngt_amd_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
+  }
+  return 0;
+}
+
+extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes,
+                                            uint32_t nq, uint32_t k, double radius, uint32_t* d_ids,
+                                            float* d_dists, uint32_t* d_n, void* stream) {
+  if (!ix || (!d_queries && nq) || k == 0) return fail("ngt_amd_linear_search_device: bad arguments");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+  // enough slices to fill the chip: ~4 waves per CU over all queries
+  uint64_t want = ((uint64_t)ix->cu_count * 16 + nq - 1) / nq;
+  uint64_t maxs = (ix->nrows + 255) / 256;
+  uint32_t nslices = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxs, 1)));
+  static thread_local DevBuf<uint64_t> partial;
+  HIP_OK(partial.alloc((size_t)nq * nslices * k));
+  LinearArgs a{};
+  a.rows = ix->rows.p;
+  a.row_bytes = ix->row_bytes;
+  a.nrows = ix->nrows;
+  a.dp = (int)ix->dp;
+  a.valid = ix->valid.p;
+  a.queries = static_cast<const uint8_t*>(d_queries);
+  a.query_bytes = query_bytes;
+  a.nq = nq;
+  a.k = k;
+  a.radius = radius;
+  a.partial = partial.p;
+  a.out_ids = d_ids;
+  a.out_dists = d_dists;
+  a.out_n = d_n;
+  HIP_OK(launch_linear_search(a, ix->metric, ix->otype, nslices, s));
+  return 0;
+}
+
+extern "C" int ngt_amd_linear_search(ngt_amd_index* ix, const void* queries, uint32_t nq, uint32_t k,
+                                     double radius, uint32_t* ids, float* dists, uint32_t* n) {
+  if (!ix || (!queries && nq) || !ids || !dists || !n || k == 0) return fail("ngt_amd_linear_search: bad arguments");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = ix->stream;
+  DevBuf<float> raw;
+  DevBuf<uint8_t> q;
+  if (upload_queries(ix, queries, nq, raw, q, s)) return -1;
+  DevBuf<uint32_t> d_ids, d_n;
+  DevBuf<float> d_dists;
+  HIP_OK(d_ids.alloc((size_t)nq * k));
+  HIP_OK(d_dists.alloc((size_t)nq * k));
+  HIP_OK(d_n.alloc(nq));
+  if (ngt_amd_linear_search_device(ix, q.p, ix->row_bytes, nq, k, radius, d_ids.p, d_dists.p, d_n.p, s))
+    return -1;
+  HIP_OK(hipMemcpyAsync(ids, d_ids.p, (size_t)nq * k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(dists, d_dists.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(n, d_n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int ngt_amd_distances(ngt_amd_index* ix, const void* queries, uint32_t nq, const uint32_t* qidx,
+                                 const uint32_t* oid, uint64_t npairs, float* out) {
+  // queries are taken as prepared objects: [nq][padded dim] of the object type
+  // (the comparator compares two allocated objects, PrimitiveComparator.h:650-752).
+  if (!ix || !queries || !qidx || !oid || !out) return fail("ngt_amd_distances: bad arguments");
+  if (npairs == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  for (uint64_t i = 0; i < npairs; i++) {
+    if (qidx[i] >= nq) return fail("ngt_amd_distances: query index %u out of range", qidx[i]);
+    if (oid[i] >= ix->nrows) return fail("ngt_amd_distances: object id %u out of range", oid[i]);
+  }
+  hipStream_t s = ix->stream;
+  DevBuf<uint8_t> q;
+  HIP_OK(q.upload(static_cast<const uint8_t*>(queries), (size_t)nq * ix->row_bytes));
+  DevBuf<uint32_t> dq, dobj;
+  DevBuf<float> dout;
+  HIP_OK(dq.upload(qidx, npairs));
+  HIP_OK(dobj.upload(oid, npairs));
+  HIP_OK(dout.alloc(npairs));
+  DistanceArgs a{};
+  a.rows = ix->rows.p;
+  a.row_bytes = ix->row_bytes;
+  a.queries = q.p;
+  a.query_bytes = ix->row_bytes;
+  a.qidx = dq.p;
+  a.oid = dobj.p;
+  a.out = dout.p;
+  a.npairs = npairs;
+  a.dp = (int)ix->dp;
+  HIP_OK(launch_distances(a, ix->metric, ix->otype, s));
+  HIP_OK(hipMemcpyAsync(out, dout.p, npairs * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}

@@ -1,0 +1,101 @@
+// ngt_kernels.h -- argument blocks and launchers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ngt_amd {
+
+struct DistanceArgs {
+  const uint8_t* rows;     // padded object rows, row_bytes apart (row 0 = dummy)
+  uint64_t row_bytes;
+  const uint8_t* queries;  // padded query rows, query_bytes apart
+  uint64_t query_bytes;
+  const uint32_t* qidx;    // per pair: query index
+  const uint32_t* oid;     // per pair: object id
+  float* out;
+  uint64_t npairs;
+  int dp;                  // padded dimension (elements)
+};
+
+struct TreeSeedArgs {
+  const uint8_t* queries;
+  uint64_t query_bytes;
+  uint32_t nq;
+  int dp;
+  uint64_t row_bytes;            // pivot row stride
+  const uint8_t* in_pivot;       // [n_internal][row_bytes]
+  const uint32_t* in_child;      // [n_internal][children] raw Node::ID
+  const float* in_border;        // [n_internal][children-1]
+  uint32_t children;
+  uint32_t root;                 // raw Node::ID of the root
+  const uint64_t* leaf_off;      // [n_leaf+1]
+  const uint32_t* leaf_ids;
+  uint32_t seed_size;            // property.seedSize (0 => k)
+  uint32_t k;
+  int all_leaf_nodes;            // sc.useAllNodesInLeaf / SeedTypeAllLeafNodes
+  uint32_t* seeds;               // [nq][seed_stride]
+  uint32_t seed_stride;
+  uint32_t* seed_count;          // [nq]
+  uint32_t* tree_ndist;          // [nq] or null
+};
+
+struct SearchArgs {
+  const uint8_t* rows;
+  uint64_t row_bytes;
+  uint32_t nrows;
+  int dp;
+  const uint64_t* edge_off;      // CSR [nrows+1]
+  const uint32_t* edges;
+  const uint8_t* queries;
+  uint64_t query_bytes;
+  uint32_t nq;
+  // seeds: either CSR (seed_off != null) or fixed stride + counts
+  const uint32_t* seeds;
+  const uint64_t* seed_off;
+  uint32_t seed_stride;
+  const uint32_t* seed_count;
+  uint32_t k;
+  float coef;                    // explorationCoefficient = epsilon + 1 (float)
+  float radius;                  // sc.radius
+  uint64_t edge_size;            // resolved getEdgeSize()
+  uint32_t ht_log2;              // visited hash capacity (log2)
+  uint32_t cq_cap;               // unchecked LDS capacity
+  uint32_t* out_ids;             // [nq][k]
+  float* out_dists;              // [nq][k]
+  uint32_t* out_n;               // [nq]
+  uint64_t* counters;            // [nq][4]: distances, visits, expansions, overflow
+  uint32_t* work;                // work counter (zeroed before launch)
+  uint32_t* bitmap;              // [slots][bitmap_words], zero
+  uint64_t bitmap_words;
+  uint64_t* spill;               // [slots][spill_cap]
+  uint32_t spill_cap;
+  int* error;
+};
+
+struct LinearArgs {
+  const uint8_t* rows;
+  uint64_t row_bytes;
+  uint64_t nrows;
+  int dp;
+  const uint8_t* valid;          // [nrows] or null
+  const uint8_t* queries;
+  uint64_t query_bytes;
+  uint32_t nq;
+  uint32_t k;
+  double radius;                 // < 0 => unbounded
+  uint64_t* partial;             // [nq][nslices][k]
+  uint32_t* out_ids;
+  float* out_dists;
+  uint32_t* out_n;
+};
+
+hipError_t launch_distances(const DistanceArgs& a, int metric, int otype, hipStream_t s);
+hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipStream_t s);
+size_t search_lds_bytes(const SearchArgs& a, int otype);
+hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,
+                               hipStream_t s);
+hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint32_t nslices,
+                                hipStream_t s);
+
+}  // namespace ngt_amd

@@ -1,0 +1,619 @@
+// search_kernels.hip -- gfx950 kernels for the NGT distance hot path.
+//
+//  * ngt_distances_kernel   : batched comparator (query x candidate-id list),
+//                             the batch form of PrimitiveComparator::*::compare.
+//  * ngt_tree_seed_kernel   : GraphAndTreeIndex::getSeedsFromTree
+//                             (lib/NGT/Index.h:1524-1567) -- DVP-tree leaf
+//                             descent + srand(leafID) thinning, one wave/query.
+//  * ngt_graph_search_kernel: NeighborhoodGraph::searchReadOnlyGraph
+//                             (lib/NGT/Graph.cpp:398-495), one wave per query,
+//                             persistent over a query work counter.
+//  * ngt_linear_search_kernel + merge: ObjectSpaceRepository::linearSearch
+//                             (lib/NGT/ObjectSpaceRepository.h:466-502).
+//
+// All per-query state of the best-first search lives in LDS:
+//   visited set   : open-addressing hash of object ids (exact; spills to a
+//                   per-slot HBM bitmap when it fills),
+//   unchecked set : unsorted array of (dist,id) keys; pop = wave min-reduce;
+//                   entries farther than the exploration radius are dead and
+//                   are dropped on compaction (they could only terminate the
+//                   loop, Graph.cpp:433-435); spills to HBM when full,
+//   results       : sorted array of the k best keys.
+// The accept step runs in neighbour order with wave-uniform radius updates,
+// so the traversal is the reference's, not an approximation of it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ngt_device.h"
+#include "ngt_kernels.h"
+
+namespace ngt_amd {
+
+// ---------------------------------------------------------------------------
+// glibc random(3) TYPE_3, for srand(leafID) (lib/NGT/Index.h:1555-1559).
+// ---------------------------------------------------------------------------
+struct GlibcRand {
+  uint32_t s[31];
+  int f, r;
+  __device__ void seed(uint32_t sd) {
+    int32_t word = (int32_t)(sd == 0 ? 1u : sd);
+    s[0] = (uint32_t)word;
+    for (int i = 1; i < 31; i++) {
+      int32_t hi = word / 127773, lo = word % 127773;
+      word = 16807 * lo - 2836 * hi;
+      if (word < 0) word += 2147483647;
+      s[i] = (uint32_t)word;
+    }
+    f = 3;
+    r = 0;
+    for (int i = 0; i < 310; i++) next();
+  }
+  __device__ int next() {
+    s[f] += s[r];
+    int res = (int)((s[f] >> 1) & 0x7fffffff);
+    f = f == 30 ? 0 : f + 1;
+    r = r == 30 ? 0 : r + 1;
+    return res;
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ const T* row_ptr(const uint8_t* rows, uint64_t row_bytes, uint32_t id) {
+  return reinterpret_cast<const T*>(rows + (uint64_t)id * row_bytes);
+}
+
+// Copy a padded query row (dp elements) into LDS with 16-byte stores.
+template <typename T>
+__device__ __forceinline__ void load_query(T* qlds, const uint8_t* src, int dp) {
+  const int n16 = (dp * (int)sizeof(T)) >> 4;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(qlds);
+  for (int i = lane_id(); i < n16; i += 64) d[i] = s[i];
+}
+
+// Distances for `m` candidate ids staged in LDS; 16 rows per wave step,
+// 4 lanes per row.  Results land in dists[0..m).
+template <int M, typename T>
+__device__ __forceinline__ void eval_batch(const T* qlds, const uint8_t* rows, uint64_t row_bytes,
+                                           int dp, const uint32_t* ids, float* dists, int m) {
+  const int lane = lane_id();
+  const int g = lane & 3;
+  for (int r0 = 0; r0 < m; r0 += 16) {
+    const int r = r0 + (lane >> 2);
+    if (r < m) {
+      const float d = quad_distance<M, T>(qlds, row_ptr<T>(rows, row_bytes, ids[r]), dp, g);
+      if (g == 0) dists[r] = d;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Batched comparator.  pair i: (query qidx[i], object oid[i]) -> out[i].
+// ---------------------------------------------------------------------------
+template <int M, typename T>
+__global__ void __launch_bounds__(256) ngt_distances_kernel(DistanceArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane & 3;
+  const uint64_t quad = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+  for (uint64_t i = quad; i < a.npairs; i += nquads) {
+    const T* q = reinterpret_cast<const T*>(a.queries + (uint64_t)a.qidx[i] * a.query_bytes);
+    const T* x = row_ptr<T>(a.rows, a.row_bytes, a.oid[i]);
+    const float d = quad_distance<M, T>(q, x, a.dp, g);
+    if (g == 0) a.out[i] = d;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tree seeds: one wave per query.
+// ---------------------------------------------------------------------------
+template <int M, typename T>
+__global__ void __launch_bounds__(64) ngt_tree_seed_kernel(TreeSeedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  T* qlds = reinterpret_cast<T*>(smem);
+  const int lane = lane_id();
+  for (uint32_t qi = blockIdx.x; qi < a.nq; qi += gridDim.x) {
+    load_query<T>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
+    __syncthreads();
+    uint32_t node = a.root;
+    uint32_t ndist = 0;
+    // DVPTree::search leaf mode, radius 0 (Tree.cpp:400-480, 531-563)
+    while (!(node & 0x80000000u)) {
+      const uint32_t iid = node & 0x7fffffffu;
+      float d = 0.f;
+      if (lane < 4) d = quad_distance<M, T>(qlds, row_ptr<T>(a.in_pivot, a.row_bytes, iid), a.dp, lane);
+      d = __shfl(d, 0, 64);
+      ndist++;
+      const float* borders = a.in_border + (uint64_t)iid * (a.children - 1);
+      uint32_t mid = 0;
+      for (; mid < a.children - 1; mid++)
+        if (d < borders[mid]) break;
+      node = a.in_child[(uint64_t)iid * a.children + mid];
+    }
+    const uint32_t lid = node & 0x7fffffffu;
+    const uint64_t b = a.leaf_off[lid], e = a.leaf_off[lid + 1];
+    uint32_t n = (uint32_t)(e - b);
+    uint32_t* out = a.seeds + (uint64_t)qi * a.seed_stride;
+    if (n > a.seed_stride) n = a.seed_stride;
+    for (uint32_t i = lane; i < n; i += 64) out[i] = a.leaf_ids[b + i];
+    __syncthreads();
+    uint32_t ss = a.seed_size == 0 ? a.k : a.seed_size;
+    if (ss > a.k) ss = a.k;
+    if (a.all_leaf_nodes) ss = n;
+    if (lane == 0) {
+      if (n > ss) {
+        // thinning (Index.h:1555-1562)
+        GlibcRand rnd;
+        rnd.seed(lid);
+        for (uint32_t i = n; i > ss; i--) {
+          double random = ((double)rnd.next() + 1.0) / ((double)2147483647 + 2.0);
+          uint32_t idx = (uint32_t)floor((double)i * random);
+          out[idx] = out[i - 1];
+        }
+        n = ss;
+      }
+      a.seed_count[qi] = n;
+      if (a.tree_ndist) a.tree_ndist[qi] = ndist;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Graph search.
+// ---------------------------------------------------------------------------
+struct SearchState {
+  uint32_t* ht;      // visited hash (LDS)
+  uint64_t* cq;      // unchecked keys (LDS)
+  uint64_t* res;     // sorted results (LDS)
+  uint32_t* nid;     // staged candidate ids (LDS, 64)
+  float* nd;         // staged distances (LDS, 64)
+};
+
+__device__ __forceinline__ uint32_t ht_hash(uint32_t id, uint32_t shift) {
+  return (id * 0x9E3779B1u) >> shift;
+}
+
+// Insert `id` into the visited set; true if it was not present.
+__device__ __forceinline__ bool visit(const SearchArgs& a, SearchState& st, uint32_t id,
+                                      bool bitmap_mode, uint32_t* bitmap) {
+  if (bitmap_mode) {
+    const uint32_t bit = 1u << (id & 31);
+    const uint32_t old = atomicOr(bitmap + (id >> 5), bit);
+    return !(old & bit);
+  }
+  const uint32_t mask = (1u << a.ht_log2) - 1;
+  uint32_t h = ht_hash(id, 32 - a.ht_log2);
+  for (;;) {
+    const uint32_t old = atomicCAS(st.ht + h, 0u, id);
+    if (old == 0u) return true;
+    if (old == id) return false;
+    h = (h + 1) & mask;
+  }
+}
+
+// Move the LDS hash contents into the per-slot HBM bitmap (exact overflow path).
+__device__ void ht_to_bitmap(const SearchArgs& a, SearchState& st, uint32_t* bitmap) {
+  const uint32_t n = 1u << a.ht_log2;
+  for (uint32_t i = lane_id(); i < n; i += 64) {
+    const uint32_t id = st.ht[i];
+    if (id) atomicOr(bitmap + (id >> 5), 1u << (id & 31));
+  }
+  __threadfence_block();
+}
+
+// Sorted insert of `key` into res[0..nres) keeping at most k entries.
+__device__ __forceinline__ void res_insert(uint64_t* res, uint32_t& nres, uint32_t k, uint64_t key) {
+  const int lane = lane_id();
+  uint32_t lt = 0;
+  for (uint32_t i = lane; i < nres; i += 64) lt += res[i] < key ? 1u : 0u;
+  const uint32_t pos = wave_sum_u32(lt);
+  if (pos >= k) return;
+  const uint32_t last = nres < k - 1 ? nres : k - 1;  // [pos, last) moves up one
+  if (last > pos) {
+    for (int c = (int)((last - 1) >> 6); c >= (int)(pos >> 6); c--) {
+      const uint32_t i = (uint32_t)c * 64 + lane;
+      uint64_t v = 0;
+      const bool mv = i >= pos && i < last;
+      if (mv) v = res[i];
+      __builtin_amdgcn_wave_barrier();
+      if (mv) res[i + 1] = v;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (lane == 0) res[pos] = key;
+  __builtin_amdgcn_wave_barrier();
+  nres = nres + 1 < k ? nres + 1 : k;
+}
+
+// Drop unchecked entries farther than expR (they can never be expanded).
+__device__ __forceinline__ uint32_t compact(uint64_t* v, uint32_t n, float expr) {
+  const int lane = lane_id();
+  uint32_t out = 0;
+  for (uint32_t b = 0; b < n; b += 64) {
+    const uint32_t i = b + lane;
+    uint64_t key = i < n ? v[i] : ~0ull;
+    const bool keep = i < n && key_dist(key) <= expr;
+    const uint64_t mask = ballot64(keep);
+    __builtin_amdgcn_wave_barrier();
+    if (keep) v[out + mbcnt(mask)] = key;
+    __builtin_amdgcn_wave_barrier();
+    out += (uint32_t)__popcll(mask);
+  }
+  return out;
+}
+
+template <int M, typename T>
+__global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = lane_id();
+  SearchState st;
+  uint8_t* p = smem;
+  st.ht = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)4 << a.ht_log2;
+  st.cq = reinterpret_cast<uint64_t*>(p);
+  p += (size_t)8 * a.cq_cap;
+  st.res = reinterpret_cast<uint64_t*>(p);
+  p += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
+  st.nid = reinterpret_cast<uint32_t*>(p);
+  p += 256;
+  st.nd = reinterpret_cast<float*>(p);
+  p += 256;
+  T* qlds = reinterpret_cast<T*>(p);
+
+  const uint32_t slot = blockIdx.x;
+  uint32_t* bitmap = a.bitmap + (uint64_t)slot * a.bitmap_words;
+  uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
+  const uint32_t hcap = 1u << a.ht_log2;
+  const uint32_t hlimit = hcap - (hcap >> 2);  // 75 % load factor
+
+  for (;;) {
+    uint32_t qi = 0;
+    if (lane == 0) qi = atomicAdd(a.work, 1u);
+    qi = __shfl(qi, 0, 64);
+    if (qi >= a.nq) break;
+
+    // ---- per-query init -----------------------------------------------
+    for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
+    load_query<T>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
+    __syncthreads();
+
+    bool bitmap_mode = false;
+    uint32_t nvisited = 0;
+    uint32_t ncq = 0, nspill = 0, nres = 0;
+    uint64_t ndist = 0, nvisit = 0, nexp = 0;
+    float radius = a.radius;
+    const uint32_t k = a.k;
+
+    // ---- setupDistances + setupSeeds (Graph.cpp:293-367) ----------------
+    const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
+    const uint32_t ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
+    for (uint32_t base = 0; base < ns; base += 64) {
+      const uint32_t m = ns - base < 64 ? ns - base : 64;
+      if ((uint32_t)lane < m) st.nid[lane] = a.seeds[sb + base + lane];
+      __syncthreads();
+      eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, st.nid, st.nd, (int)m);
+      __syncthreads();
+      if ((uint32_t)lane < m) {
+        const uint32_t id = st.nid[lane];
+        const uint64_t key = make_key(st.nd[lane], id);
+        visit(a, st, id, bitmap_mode, bitmap);
+        if (ncq + lane < a.cq_cap) st.cq[ncq + lane] = key;
+        else spill[nspill + (ncq + lane - a.cq_cap)] = key;
+      }
+      __syncthreads();
+      // results take the k best seeds with d <= radius (sorted order, :347-353)
+      for (uint32_t j = 0; j < m; j++) {
+        const float d = st.nd[j];
+        if (d <= a.radius) res_insert(st.res, nres, k, make_key(d, st.nid[j]));
+      }
+      const uint32_t add = m;
+      if (ncq + add <= a.cq_cap) {
+        ncq += add;
+      } else {
+        nspill += ncq + add - a.cq_cap;
+        ncq = a.cq_cap;
+      }
+      ndist += m;
+      nvisited += m;
+      __syncthreads();
+      if (!bitmap_mode && nvisited > hlimit) {
+        ht_to_bitmap(a, st, bitmap);
+        bitmap_mode = true;
+        __syncthreads();
+      }
+    }
+    if (nres >= k) radius = key_dist(st.res[k - 1]);
+    float expr = __fmul_rn(a.coef, radius);
+
+    // ---- best-first loop (Graph.cpp:430-486) ----------------------------
+    for (;;) {
+      // pop the minimum key
+      uint64_t best = ~0ull;
+      uint32_t bidx = 0xffffffffu;
+      for (uint32_t i = lane; i < ncq; i += 64) {
+        const uint64_t key = st.cq[i];
+        if (key < best) { best = key; bidx = i; }
+      }
+      for (uint32_t i = lane; i < nspill; i += 64) {
+        const uint64_t key = spill[i];
+        if (key < best) { best = key; bidx = i | 0x80000000u; }
+      }
+      const uint64_t wbest = wave_min_u64(best);
+      if (wbest == ~0ull) break;
+      const uint64_t owner = ballot64(best == wbest);
+      const int olane = __ffsll((long long)owner) - 1;
+      bidx = __shfl(bidx, olane, 64);
+      if (key_dist(wbest) > expr) break;
+      if (lane == 0) {
+        if (bidx & 0x80000000u) spill[bidx & 0x7fffffffu] = spill[nspill - 1];
+        else st.cq[bidx] = st.cq[ncq - 1];
+      }
+      if (bidx & 0x80000000u) nspill--; else ncq--;
+      __syncthreads();
+      nexp++;
+
+      const uint32_t target = key_id(wbest);
+      const uint64_t eb = a.edge_off[target];
+      uint64_t deg = a.edge_off[target + 1] - eb;
+      if (deg > a.edge_size) deg = a.edge_size;
+
+      for (uint64_t base = 0; base < deg; base += 64) {
+        const uint32_t cnt = (uint32_t)(deg - base < 64 ? deg - base : 64);
+        bool fresh = false;
+        uint32_t id = 0;
+        if ((uint32_t)lane < cnt) {
+          id = a.edges[eb + base + lane];
+          fresh = visit(a, st, id, bitmap_mode, bitmap);
+        }
+        const uint64_t fmask = ballot64(fresh);
+        const uint32_t m = (uint32_t)__popcll(fmask);
+        if (fresh) st.nid[mbcnt(fmask)] = id;
+        nvisited += m;
+        __syncthreads();
+        if (m == 0) continue;
+        eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, st.nid, st.nd, (int)m);
+        __syncthreads();
+        ndist += m;
+        nvisit += m;
+        // accept in neighbour order (Graph.cpp:471-483); only candidates
+        // within the radius at batch start can be accepted.
+        uint64_t okmask = ballot64((uint32_t)lane < m && st.nd[lane] <= expr);
+        while (okmask) {
+          const int j = __ffsll((long long)okmask) - 1;
+          okmask &= okmask - 1;
+          const float d = st.nd[j];
+          if (!(d <= expr)) continue;
+          const uint64_t key = make_key(d, st.nid[j]);
+          if (ncq >= a.cq_cap) {
+            ncq = compact(st.cq, ncq, expr);
+            if (nspill) {
+              nspill = compact(spill, nspill, expr);
+            }
+          }
+          if (ncq < a.cq_cap) {
+            if (lane == 0) st.cq[ncq] = key;
+            ncq++;
+          } else {
+            if (nspill >= a.spill_cap) {
+              if (lane == 0) atomicOr(a.error, 1);
+            } else {
+              if (lane == 0) spill[nspill] = key;
+              nspill++;
+            }
+          }
+          if (d <= radius) {
+            res_insert(st.res, nres, k, key);
+            if (nres >= k) {
+              radius = key_dist(st.res[k - 1]);
+              expr = __fmul_rn(a.coef, radius);
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        // exact overflow of the visited set into the HBM bitmap
+        if (!bitmap_mode && nvisited > hlimit) {
+          ht_to_bitmap(a, st, bitmap);
+          bitmap_mode = true;
+          __syncthreads();
+        }
+      }
+    }
+
+    // ---- results (moveFrom: ascending (distance, id), ObjectSpace.h:49-57)
+    for (uint32_t i = lane; i < nres; i += 64) {
+      a.out_ids[(uint64_t)qi * a.k + i] = key_id(st.res[i]);
+      a.out_dists[(uint64_t)qi * a.k + i] = key_dist(st.res[i]);
+    }
+    if (lane == 0) {
+      a.out_n[qi] = nres;
+      if (a.counters) {
+        a.counters[(uint64_t)qi * 4 + 0] = ndist;
+        a.counters[(uint64_t)qi * 4 + 1] = nvisit;
+        a.counters[(uint64_t)qi * 4 + 2] = nexp;
+        a.counters[(uint64_t)qi * 4 + 3] = bitmap_mode ? 1 : 0;
+      }
+    }
+    if (bitmap_mode) {
+      // leave the slot's bitmap clean for the next query
+      uint4* bm = reinterpret_cast<uint4*>(bitmap);
+      const uint64_t n16 = a.bitmap_words / 4;
+      for (uint64_t i = lane; i < n16; i += 64) bm[i] = make_uint4(0, 0, 0, 0);
+      __threadfence_block();
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Linear search: block (slice s, query q) keeps a sorted top-k of its slice;
+// a merge kernel combines the slices.
+// ---------------------------------------------------------------------------
+template <int M, typename T>
+__global__ void __launch_bounds__(64) ngt_linear_search_kernel(LinearArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = lane_id();
+  uint64_t* res = reinterpret_cast<uint64_t*>(smem);
+  uint8_t* p = smem + (((size_t)8 * (a.k + 1) + 15) & ~(size_t)15);
+  uint32_t* nid = reinterpret_cast<uint32_t*>(p);
+  float* nd = reinterpret_cast<float*>(p + 256);
+  T* qlds = reinterpret_cast<T*>(p + 512);
+  const uint32_t qi = blockIdx.y;
+  const uint32_t slice = blockIdx.x;
+  load_query<T>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
+  __syncthreads();
+  const uint64_t per = (a.nrows + gridDim.x - 1) / gridDim.x;
+  uint64_t b = (uint64_t)slice * per, e = b + per;
+  if (b < 1) b = 1;
+  if (e > a.nrows) e = a.nrows;
+  uint32_t nres = 0;
+  float thr = __int_as_float(0x7f800000);  // +inf: nothing to beat yet
+  for (uint64_t base = b; base < e; base += 64) {
+    const uint32_t cnt = (uint32_t)(e - base < 64 ? e - base : 64);
+    const uint32_t id = (uint32_t)(base + lane);
+    const bool ok = (uint32_t)lane < cnt && (a.valid == nullptr || a.valid[id]);
+    const uint64_t mask = ballot64(ok);
+    const uint32_t m = (uint32_t)__popcll(mask);
+    if (ok) nid[mbcnt(mask)] = id;
+    __syncthreads();
+    eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, nid, nd, (int)m);
+    __syncthreads();
+    // (radius < 0 || d <= radius), then bounded max-heap == k best (d, id)
+    uint64_t cand = ballot64((uint32_t)lane < m && (a.radius < 0.0 || (double)nd[lane] <= a.radius) &&
+                            (nres < a.k || nd[lane] <= thr));
+    while (cand) {
+      const int j = __ffsll((long long)cand) - 1;
+      cand &= cand - 1;
+      const uint64_t key = make_key(nd[j], nid[j]);
+      if (nres >= a.k && key > res[a.k - 1]) continue;
+      res_insert(res, nres, a.k, key);
+      if (nres >= a.k) thr = key_dist(res[a.k - 1]);
+    }
+    __syncthreads();
+  }
+  uint64_t* out = a.partial + ((uint64_t)qi * gridDim.x + slice) * a.k;
+  for (uint32_t i = lane; i < a.k; i += 64) out[i] = i < nres ? res[i] : ~0ull;
+}
+
+__global__ void __launch_bounds__(64) ngt_linear_merge_kernel(LinearArgs a, uint32_t nslices) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t* res = reinterpret_cast<uint64_t*>(smem);
+  const int lane = lane_id();
+  const uint32_t qi = blockIdx.x;
+  uint32_t nres = 0;
+  const uint64_t* part = a.partial + (uint64_t)qi * nslices * a.k;
+  for (uint64_t base = 0; base < (uint64_t)nslices * a.k; base += 64) {
+    const uint64_t i = base + lane;
+    const uint64_t key = i < (uint64_t)nslices * a.k ? part[i] : ~0ull;
+    uint64_t cand = ballot64(key != ~0ull && (nres < a.k || key < res[a.k - 1]));
+    while (cand) {
+      const int j = __ffsll((long long)cand) - 1;
+      cand &= cand - 1;
+      const uint64_t kj = __shfl(key, j, 64);
+      if (nres >= a.k && kj > res[a.k - 1]) continue;
+      res_insert(res, nres, a.k, kj);
+    }
+  }
+  for (uint32_t i = lane; i < nres; i += 64) {
+    a.out_ids[(uint64_t)qi * a.k + i] = key_id(res[i]);
+    a.out_dists[(uint64_t)qi * a.k + i] = key_dist(res[i]);
+  }
+  if (lane == 0) a.out_n[qi] = nres;
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (dispatch on metric x object type).
+// ---------------------------------------------------------------------------
+#define NGT_DISPATCH(METRIC, OTYPE, LAUNCH)                                    \
+  do {                                                                         \
+    if ((OTYPE) == kFloat) {                                                   \
+      switch (METRIC) {                                                        \
+        case kL1: LAUNCH(kL1, float); break;                                   \
+        case kL2: LAUNCH(kL2, float); break;                                   \
+        case kHamming: LAUNCH(kHamming, float); break;                         \
+        case kAngle: LAUNCH(kAngle, float); break;                             \
+        case kCosine: LAUNCH(kCosine, float); break;                           \
+        case kNormalizedAngle: LAUNCH(kNormalizedAngle, float); break;         \
+        case kNormalizedCosine: LAUNCH(kNormalizedCosine, float); break;       \
+        case kJaccard: LAUNCH(kJaccard, float); break;                         \
+        case kSparseJaccard: LAUNCH(kSparseJaccard, float); break;             \
+        case kNormalizedL2: LAUNCH(kNormalizedL2, float); break;               \
+        case kPoincare: LAUNCH(kPoincare, float); break;                       \
+        case kLorentz: LAUNCH(kLorentz, float); break;                         \
+        default: return hipErrorInvalidValue;                                  \
+      }                                                                        \
+    } else if ((OTYPE) == kUint8) {                                            \
+      switch (METRIC) {                                                        \
+        case kL1: LAUNCH(kL1, uint8_t); break;                                 \
+        case kL2: LAUNCH(kL2, uint8_t); break;                                 \
+        case kHamming: LAUNCH(kHamming, uint8_t); break;                       \
+        case kAngle: LAUNCH(kAngle, uint8_t); break;                           \
+        case kCosine: LAUNCH(kCosine, uint8_t); break;                         \
+        case kNormalizedAngle: LAUNCH(kNormalizedAngle, uint8_t); break;       \
+        case kNormalizedCosine: LAUNCH(kNormalizedCosine, uint8_t); break;     \
+        case kJaccard: LAUNCH(kJaccard, uint8_t); break;                       \
+        case kNormalizedL2: LAUNCH(kNormalizedL2, uint8_t); break;             \
+        case kPoincare: LAUNCH(kPoincare, uint8_t); break;                     \
+        case kLorentz: LAUNCH(kLorentz, uint8_t); break;                       \
+        default: return hipErrorInvalidValue;                                  \
+      }                                                                        \
+    } else {                                                                   \
+      return hipErrorInvalidValue;                                             \
+    }                                                                          \
+  } while (0)
+
+hipError_t launch_distances(const DistanceArgs& a, int metric, int otype, hipStream_t s) {
+  if (a.npairs == 0) return hipSuccess;
+  uint64_t blocks = (a.npairs * 4 + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+#define L_DIST(MM, TT) hipLaunchKernelGGL((ngt_distances_kernel<MM, TT>), dim3((uint32_t)blocks), dim3(256), 0, s, a)
+  NGT_DISPATCH(metric, otype, L_DIST);
+#undef L_DIST
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
+  uint32_t blocks = a.nq < 8192 ? a.nq : 8192;
+#define L_TREE(MM, TT) hipLaunchKernelGGL((ngt_tree_seed_kernel<MM, TT>), dim3(blocks), dim3(64), lds, s, a)
+  NGT_DISPATCH(metric, otype, L_TREE);
+#undef L_TREE
+  return hipGetLastError();
+}
+
+size_t search_lds_bytes(const SearchArgs& a, int otype) {
+  size_t b = ((size_t)4 << a.ht_log2) + (size_t)8 * a.cq_cap;
+  b += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
+  b += 512;
+  b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
+  return b;
+}
+
+hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,
+                               hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = search_lds_bytes(a, otype);
+#define L_SEARCH(MM, TT) hipLaunchKernelGGL((ngt_graph_search_kernel<MM, TT>), dim3(slots), dim3(64), lds, s, a)
+  NGT_DISPATCH(metric, otype, L_SEARCH);
+#undef L_SEARCH
+  return hipGetLastError();
+}
+
+hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint32_t nslices,
+                                hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = (((size_t)8 * (a.k + 1) + 15) & ~(size_t)15) + 512 +
+                     (((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15);
+#define L_LIN(MM, TT) hipLaunchKernelGGL((ngt_linear_search_kernel<MM, TT>), dim3(nslices, a.nq), dim3(64), lds, s, a)
+  NGT_DISPATCH(metric, otype, L_LIN);
+#undef L_LIN
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t lds2 = ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
+  hipLaunchKernelGGL(ngt_linear_merge_kernel, dim3(a.nq), dim3(64), lds2, s, a, nslices);
+  return hipGetLastError();
+}
+
+}  // namespace ngt_amd

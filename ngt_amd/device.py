@@ -1,0 +1,172 @@
+"""Thin wrapper over the batched C ABI of include/ngt_amd.h.
+
+``DeviceIndex`` holds an index resident in HBM (padded row-major object slab,
+CSR adjacency, optional DVP tree) and exposes the batched hot path:
+``search`` (best-first graph search), ``linear_search`` and ``distances``.
+Host arrays are numpy; the ``*_device`` forms take raw device pointers (e.g.
+``torch.Tensor.data_ptr()`` of tensors on ``cuda:N``) and a HIP stream handle.
+"""
+import ctypes
+from ctypes import byref, c_void_p
+
+import numpy as np
+
+from . import NativeError, lib
+from ._sigs import SearchParams
+
+DISTANCE = {
+    "l1": 0, "l2": 1, "hamming": 2, "angle": 3, "cosine": 4, "normalized_angle": 5,
+    "normalized_cosine": 6, "jaccard": 7, "sparse_jaccard": 8, "normalized_l2": 9,
+    "poincare": 100, "lorentz": 101,
+}
+SEED_TREE, SEED_GIVEN, SEED_RANDOM = 0, 1, 2
+COUNTERS = 4
+
+
+def padded_dim(dim):
+    return ((dim - 1) // 16 + 1) * 16
+
+
+def _chk(rc):
+    if rc != 0:
+        raise NativeError(lib().ngt_amd_last_error().decode())
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None else None
+
+
+class DeviceIndex(object):
+    def __init__(self, distance="l2", object_type="float", dim=128, device=0):
+        self.L = lib()
+        self.metric = DISTANCE[distance] if isinstance(distance, str) else int(distance)
+        self.otype = 2 if object_type in ("float", "f", 2) else 1
+        self.dtype = np.float32 if self.otype == 2 else np.uint8
+        self.dim = dim
+        self.dp = padded_dim(dim)
+        h = c_void_p()
+        _chk(self.L.ngt_amd_index_create(byref(h), device, self.metric, self.otype, dim))
+        self.h = h
+        self.nrows = 0
+
+    # ---- data -------------------------------------------------------------
+    def set_objects(self, rows, valid=None):
+        """rows: [nrows, dim or padded dim] with row 0 the dummy slot."""
+        rows = np.asarray(rows, dtype=self.dtype)
+        if rows.shape[1] != self.dp:
+            p = np.zeros((rows.shape[0], self.dp), self.dtype)
+            p[:, :rows.shape[1]] = rows
+            rows = p
+        rows = np.ascontiguousarray(rows)
+        v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+        _chk(self.L.ngt_amd_index_set_objects(self.h, rows.ctypes.data, rows.shape[0], _ptr(v)))
+        self.nrows = rows.shape[0]
+
+    def set_objects_device(self, d_rows, nrows):
+        _chk(self.L.ngt_amd_index_set_objects_device(self.h, d_rows, nrows))
+        self.nrows = nrows
+
+    def set_graph(self, offsets, edges):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        edges = np.ascontiguousarray(edges, dtype=np.uint32)
+        _chk(self.L.ngt_amd_index_set_graph(self.h, offsets.ctypes.data, edges.ctypes.data, len(edges)))
+
+    def set_graph_device(self, d_offsets, d_edges, nedges):
+        _chk(self.L.ngt_amd_index_set_graph_device(self.h, d_offsets, d_edges, nedges))
+
+    def set_tree(self, tree):
+        piv = np.ascontiguousarray(tree["in_pivot"], dtype=self.dtype)
+        if piv.shape[1] != self.dp:
+            p = np.zeros((piv.shape[0], self.dp), self.dtype)
+            p[:, :piv.shape[1]] = piv
+            piv = p
+        child = np.ascontiguousarray(tree["in_child"], dtype=np.uint32)
+        border = np.ascontiguousarray(tree["in_border"], dtype=np.float32)
+        loff = np.ascontiguousarray(tree["leaf_off"], dtype=np.uint64)
+        lids = np.ascontiguousarray(tree["leaf_ids"], dtype=np.uint32)
+        _chk(self.L.ngt_amd_index_set_tree(self.h, piv.ctypes.data, piv.shape[0], child.ctypes.data,
+                                           border.ctypes.data, child.shape[1], int(tree["root"]),
+                                           loff.ctypes.data, len(loff) - 1, lids.ctypes.data, len(lids)))
+
+    def set_search_property(self, edge_size_for_search=0, dynamic_edge_size_base=30,
+                            dynamic_edge_size_rate=20, seed_size=10, seed_type=0):
+        _chk(self.L.ngt_amd_index_set_search_property(self.h, edge_size_for_search, dynamic_edge_size_base,
+                                                      dynamic_edge_size_rate, seed_size, seed_type))
+
+    def resolve_edge_size(self, edge_size, epsilon):
+        return int(self.L.ngt_amd_resolve_edge_size(self.h, edge_size, epsilon))
+
+    # ---- hot path -----------------------------------------------------------
+    def search(self, queries, k=10, epsilon=0.1, radius=-1.0, edge_size=-1, seed_mode=SEED_TREE,
+               seeds=None, counters=True):
+        """queries: [nq, dim] float.  seeds: list of arrays for SEED_GIVEN."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        nq = q.shape[0]
+        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0)
+        ids = np.zeros((nq, k), np.uint32)
+        ds = np.zeros((nq, k), np.float32)
+        n = np.zeros(nq, np.uint32)
+        cnt = np.zeros((nq, COUNTERS), np.uint64) if counters else None
+        sp = so = None
+        if seed_mode == SEED_GIVEN:
+            so = np.zeros(nq + 1, np.uint64)
+            so[1:] = np.cumsum([len(s) for s in seeds])
+            sp = np.ascontiguousarray(np.concatenate([np.asarray(s, np.uint32) for s in seeds])
+                                      if so[-1] else np.zeros(1, np.uint32))
+        _chk(self.L.ngt_amd_search(self.h, byref(prm), q.ctypes.data, nq, _ptr(sp), _ptr(so), ids.ctypes.data,
+                                   ds.ctypes.data, n.ctypes.data, _ptr(cnt)))
+        return ids, ds, n, cnt
+
+    def search_device(self, d_queries, query_bytes, nq, d_ids, d_dists, d_n, d_counters=None, k=10,
+                      epsilon=0.1, radius=-1.0, edge_size=-1, seed_mode=SEED_TREE, d_seeds=None,
+                      d_seed_off=None, stream=None):
+        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0)
+        _chk(self.L.ngt_amd_search_device(self.h, byref(prm), d_queries, query_bytes, nq, d_seeds, d_seed_off,
+                                          d_ids, d_dists, d_n, d_counters, stream))
+
+    def last_search_kernel_ms(self):
+        return float(self.L.ngt_amd_last_search_kernel_ms(self.h))
+
+    def prepare_queries_device(self, d_in, nq, d_out, stream=None):
+        _chk(self.L.ngt_amd_prepare_queries_device(self.h, d_in, nq, d_out, stream))
+
+    def linear_search(self, queries, k=10, radius=-1.0):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        nq = q.shape[0]
+        ids = np.zeros((nq, k), np.uint32)
+        ds = np.zeros((nq, k), np.float32)
+        n = np.zeros(nq, np.uint32)
+        _chk(self.L.ngt_amd_linear_search(self.h, q.ctypes.data, nq, k, radius, ids.ctypes.data, ds.ctypes.data,
+                                          n.ctypes.data))
+        return ids, ds, n
+
+    def linear_search_device(self, d_queries, query_bytes, nq, k, d_ids, d_dists, d_n, radius=-1.0,
+                             stream=None):
+        _chk(self.L.ngt_amd_linear_search_device(self.h, d_queries, query_bytes, nq, k, radius, d_ids, d_dists,
+                                                 d_n, stream))
+
+    def distances(self, queries, qidx, oid):
+        """queries: prepared rows [nq, dim or dp] of the object type."""
+        q = np.asarray(queries, dtype=self.dtype)
+        if q.shape[1] != self.dp:
+            p = np.zeros((q.shape[0], self.dp), self.dtype)
+            p[:, :q.shape[1]] = q
+            q = p
+        q = np.ascontiguousarray(q)
+        qidx = np.ascontiguousarray(qidx, dtype=np.uint32)
+        oid = np.ascontiguousarray(oid, dtype=np.uint32)
+        out = np.zeros(len(oid), np.float32)
+        _chk(self.L.ngt_amd_distances(self.h, q.ctypes.data, q.shape[0], qidx.ctypes.data, oid.ctypes.data,
+                                      len(oid), out.ctypes.data))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ngt_amd_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
