@@ -74,11 +74,11 @@ typedef struct {
   int32_t all_leaf_nodes;/* SearchContainer::useAllNodesInLeaf                      */
 } ngt_amd_search_params;
 
-/* Per-query counters written by the search (4 x uint64 per query):
+/* Per-query counters written by the search (8 x uint64 per query):
  * [0] distance computations (seeds + evaluated neighbours), [1] evaluated
  * neighbours (visitCount), [2] expanded nodes, [3] 1 if the visited set spilled
- * from LDS to the HBM bitmap. */
-#define NGT_AMD_COUNTERS_PER_QUERY 4
+ * from LDS to the HBM bitmap, [4] adjacency entries read, [5..7] reserved. */
+#define NGT_AMD_COUNTERS_PER_QUERY 8
 
 const char *ngt_amd_last_error(void);
 int ngt_amd_device_count(void);

@@ -64,7 +64,7 @@ struct SearchArgs {
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;              // [nq][k]
   uint32_t* out_n;               // [nq]
-  uint64_t* counters;            // [nq][4]: distances, visits, expansions, overflow
+  uint64_t* counters;            // [nq][8]: distances, visits, expansions, overflow, edges
   uint32_t* work;                // work counter (zeroed before launch)
   uint32_t* bitmap;              // [slots][bitmap_words], zero
   uint64_t bitmap_words;

@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
     bool bitmap_mode = false;
     uint32_t nvisited = 0;
     uint32_t ncq = 0, nspill = 0, nres = 0;
-    uint64_t ndist = 0, nvisit = 0, nexp = 0;
+    uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0;
     float radius = a.radius;
     const uint32_t k = a.k;
 
@@ -357,6 +357,7 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
       const uint64_t eb = a.edge_off[target];
       uint64_t deg = a.edge_off[target + 1] - eb;
       if (deg > a.edge_size) deg = a.edge_size;
+      nedge += deg;
 
       for (uint64_t base = 0; base < deg; base += 64) {
         const uint32_t cnt = (uint32_t)(deg - base < 64 ? deg - base : 64);
@@ -429,10 +430,15 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
     if (lane == 0) {
       a.out_n[qi] = nres;
       if (a.counters) {
-        a.counters[(uint64_t)qi * 4 + 0] = ndist;
-        a.counters[(uint64_t)qi * 4 + 1] = nvisit;
-        a.counters[(uint64_t)qi * 4 + 2] = nexp;
-        a.counters[(uint64_t)qi * 4 + 3] = bitmap_mode ? 1 : 0;
+        uint64_t* c = a.counters + (uint64_t)qi * 8;
+        c[0] = ndist;
+        c[1] = nvisit;
+        c[2] = nexp;
+        c[3] = bitmap_mode ? 1 : 0;
+        c[4] = nedge;
+        c[5] = 0;
+        c[6] = 0;
+        c[7] = 0;
       }
     }
     if (bitmap_mode) {

@@ -20,7 +20,7 @@ DISTANCE = {
     "poincare": 100, "lorentz": 101,
 }
 SEED_TREE, SEED_GIVEN, SEED_RANDOM = 0, 1, 2
-COUNTERS = 4
+COUNTERS = 8
 
 
 def padded_dim(dim):
