@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--eps", type=str, default="")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--visited", type=int, default=-1,
+                    help="visited set: -1 HBM bitmap (this workload visits ~1e5 ids/query), 0 LDS hash")
     args = ap.parse_args()
 
     import torch
@@ -225,7 +227,8 @@ def main():
     def run(eps):
         ix.search_device(qdev.data_ptr(), dp * 4, NQ, out_i.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
                          cnt.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
-                         d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=stream)
+                         d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=stream,
+                         visited_hash_log2=args.visited)
 
     # epsilon sweep (ngt eval semantics: mean recall@k over the queries)
     cands = [float(x) for x in args.eps.split(",")] if args.eps else \
@@ -313,7 +316,12 @@ def main():
                        "recall_at_10": rec, "epsilon": chosen, "edge_size": "all",
                        "graph": "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg),
                        "seeds": "getRandomSeeds (%d)" % args.seed_size,
-                       "distance_computations_per_query": U / NQ, "parallelism": "replicas x%d" % world},
+                       "distance_computations_per_query": U / NQ,
+                       "expansions_per_query": float(c[:, 2].mean()),
+                       "edges_read_per_query": E / NQ,
+                       "max_unchecked_per_query": float(c[:, 5].max()),
+                       "visited_set": "hbm-bitmap" if args.visited < 0 else "lds-hash",
+                       "parallelism": "replicas x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes},

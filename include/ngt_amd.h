@@ -72,6 +72,11 @@ typedef struct {
   int64_t edge_size;     /* SearchContainer::edgeSize: -1 property, 0 all, -2 dyn.   */
   int32_t seed_mode;     /* NGT_AMD_SEED_*                                          */
   int32_t all_leaf_nodes;/* SearchContainer::useAllNodesInLeaf                      */
+  int32_t visited_hash_log2; /* visited set: 0 = default LDS hash (2^12 ids, spills
+                                exactly to an HBM bitmap), 8..15 = LDS hash of that
+                                size, -1 = HBM bitmap from the start (for searches
+                                that visit far more ids than an LDS hash holds)  */
+  int32_t reserved;
 } ngt_amd_search_params;
 
 /* Per-query counters written by the search (8 x uint64 per query):

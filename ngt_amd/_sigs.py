@@ -5,7 +5,8 @@ from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_i
 
 class SearchParams(Structure):
     _fields_ = [("k", c_uint32), ("epsilon", c_float), ("radius", c_float), ("edge_size", c_int64),
-                ("seed_mode", c_int32), ("all_leaf_nodes", c_int32)]
+                ("seed_mode", c_int32), ("all_leaf_nodes", c_int32),
+                ("visited_hash_log2", c_int32), ("reserved", c_int32)]
 
 
 class ObjectDistance(Structure):

@@ -83,6 +83,8 @@ struct ngt_amd_index {
   DevBuf<uint64_t> edge_off;
   DevBuf<uint32_t> edges;
   uint64_t nedges = 0;
+  DevBuf<uint32_t> adj;          // padded fixed-stride copy of the adjacency
+  uint64_t adj_stride = 0;
   bool has_graph = false;
   std::vector<uint8_t> h_graph_empty;
   // tree
@@ -97,11 +99,12 @@ struct ngt_amd_index {
   int32_t dyn_base = 30, dyn_rate = 20;
   int32_t seed_size = 10, seed_type = 0;
   // scratch
-  DevBuf<uint32_t> bitmap, work, seeds, seed_count;
+  DevBuf<uint32_t> work, seeds, seed_count, slot_epoch;
+  DevBuf<uint8_t> vis;
   DevBuf<uint64_t> spill, seed_off;
   DevBuf<int> error;
   uint32_t slots = 0;
-  uint64_t bitmap_words = 0;
+  uint64_t vis_stride = 0;
   uint32_t spill_cap = 1u << 16;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -207,6 +210,23 @@ static void note_graph_empty(ngt_amd_index* ix, const uint64_t* offsets, uint64_
   for (uint64_t i = 0; i < nrows; i++) ix->h_graph_empty[i] = offsets[i + 1] == offsets[i];
 }
 
+// Padded adjacency [nrows][stride] (0-terminated rows) built on the device from
+// the CSR: one load per edge chunk instead of an offset load followed by a
+// dependent edge load.  Kept only while the widest node is <= 256 edges.
+static int build_padded_adjacency(ngt_amd_index* ix, const uint64_t* h_offsets) {
+  uint64_t maxdeg = 0;
+  for (uint64_t i = 0; i < ix->nrows; i++) maxdeg = std::max<uint64_t>(maxdeg, h_offsets[i + 1] - h_offsets[i]);
+  ix->adj.release();
+  ix->adj_stride = 0;
+  if (maxdeg == 0 || maxdeg > 256) return 0;
+  uint64_t stride = (maxdeg + 15) & ~15ull;
+  HIP_OK(ix->adj.alloc(ix->nrows * stride));
+  HIP_OK(launch_pad_adjacency(ix->edge_off.p, ix->edges.p, ix->nrows, stride, ix->adj.p, ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  ix->adj_stride = stride;
+  return 0;
+}
+
 extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offsets,
                                        const uint32_t* edges, uint64_t nedges) {
   if (!ix || !offsets || (!edges && nedges)) return fail("ngt_amd_index_set_graph: bad arguments");
@@ -221,7 +241,7 @@ extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offset
   ix->nedges = nedges;
   ix->has_graph = true;
   note_graph_empty(ix, offsets, ix->nrows);
-  return 0;
+  return build_padded_adjacency(ix, offsets);
 }
 
 extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t* d_offsets,
@@ -239,7 +259,7 @@ extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t*
   std::vector<uint64_t> h(ix->nrows + 1);
   HIP_OK(hipMemcpy(h.data(), d_offsets, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   note_graph_empty(ix, h.data(), ix->nrows);
-  return 0;
+  return build_padded_adjacency(ix, h.data());
 }
 
 extern "C" int ngt_amd_index_set_tree(ngt_amd_index* ix, const void* in_pivot, uint32_t n_internal,
@@ -298,14 +318,18 @@ static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a) {
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
   if (per_cu > 16) per_cu = 16;
   if (per_cu < 1) per_cu = 1;
-  uint32_t slots = per_cu * (uint32_t)ix->cu_count;
-  uint64_t words = ((ix->nrows + 31) / 32 + 3) & ~3ull;
-  if (slots != ix->slots || words != ix->bitmap_words || !ix->spill.p) {
-    HIP_OK(ix->bitmap.alloc((size_t)slots * words));
-    HIP_OK(hipMemset(ix->bitmap.p, 0, (size_t)slots * words * sizeof(uint32_t)));
+  uint64_t stride = (ix->nrows + 15) & ~15ull;
+  // the per-slot visited epochs take slots * nrows bytes: keep them <= 16 GiB
+  uint64_t max_slots = (16ull << 30) / stride;
+  uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * ix->cu_count, std::max<uint64_t>(max_slots, 64));
+  if (slots != ix->slots || stride != ix->vis_stride || !ix->spill.p) {
+    HIP_OK(ix->vis.alloc((size_t)slots * stride));
+    HIP_OK(hipMemset(ix->vis.p, 0, (size_t)slots * stride));
+    HIP_OK(ix->slot_epoch.alloc(slots));
+    HIP_OK(hipMemset(ix->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t)));
     HIP_OK(ix->spill.alloc((size_t)slots * ix->spill_cap));
     ix->slots = slots;
-    ix->bitmap_words = words;
+    ix->vis_stride = stride;
   }
   return 0;
 }
@@ -326,6 +350,10 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
   a.dp = (int)ix->dp;
   a.edge_off = ix->edge_off.p;
   a.edges = ix->edges.p;
+  a.adj = ix->adj.p;
+  a.adj_stride = ix->adj_stride;
+  if (const char* v = getenv("NGT_AMD_ADJ"))
+    if (atoi(v) == 0) a.adj = nullptr;
   a.queries = static_cast<const uint8_t*>(d_queries);
   a.query_bytes = query_bytes;
   a.nq = nq;
@@ -338,6 +366,8 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
   // overflow paths.
   a.ht_log2 = 12;
   a.cq_cap = 1024;
+  if (prm->visited_hash_log2 < 0) a.ht_log2 = 0;
+  else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
   if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
   if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
   a.out_ids = d_ids;
@@ -380,8 +410,9 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
     a.seed_off = d_seed_off;
   }
   if (ensure_scratch(ix, a)) return -1;
-  a.bitmap = ix->bitmap.p;
-  a.bitmap_words = ix->bitmap_words;
+  a.vis = ix->vis.p;
+  a.vis_stride = ix->vis_stride;
+  a.slot_epoch = ix->slot_epoch.p;
   a.spill = ix->spill.p;
   a.spill_cap = ix->spill_cap;
   a.work = ix->work.p;

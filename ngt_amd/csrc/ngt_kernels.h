@@ -47,6 +47,8 @@ struct SearchArgs {
   int dp;
   const uint64_t* edge_off;      // CSR [nrows+1]
   const uint32_t* edges;
+  const uint32_t* adj;           // optional padded adjacency [nrows][adj_stride], 0-terminated
+  uint64_t adj_stride;
   const uint8_t* queries;
   uint64_t query_bytes;
   uint32_t nq;
@@ -59,15 +61,16 @@ struct SearchArgs {
   float coef;                    // explorationCoefficient = epsilon + 1 (float)
   float radius;                  // sc.radius
   uint64_t edge_size;            // resolved getEdgeSize()
-  uint32_t ht_log2;              // visited hash capacity (log2)
+  uint32_t ht_log2;              // visited hash capacity (log2); 0 = HBM bitmap only
   uint32_t cq_cap;               // unchecked LDS capacity
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;              // [nq][k]
   uint32_t* out_n;               // [nq]
-  uint64_t* counters;            // [nq][8]: distances, visits, expansions, overflow, edges
+  uint64_t* counters;            // [nq][8]: distances, visits, expansions, overflow, edges, max queue
   uint32_t* work;                // work counter (zeroed before launch)
-  uint32_t* bitmap;              // [slots][bitmap_words], zero
-  uint64_t bitmap_words;
+  uint8_t* vis;                  // [slots][vis_stride] visited epochs, zero-initialised
+  uint64_t vis_stride;           // >= nrows, multiple of 16
+  uint32_t* slot_epoch;          // [slots] last epoch used by each slot
   uint64_t* spill;               // [slots][spill_cap]
   uint32_t spill_cap;
   int* error;

@@ -9,4 +9,7 @@ namespace ngt_amd {
 // metrics.  Sets *error = 2 if a normalized query is the zero vector.
 hipError_t launch_prepare_queries(const float* d_in, uint32_t dim, uint32_t nq, uint32_t dp, int otype,
                                   bool normalize, void* d_out, int* error, hipStream_t s);
+// adj[v][0..stride) = edges[off[v]..off[v+1]) followed by zeros
+hipError_t launch_pad_adjacency(const uint64_t* off, const uint32_t* edges, uint64_t nrows, uint64_t stride,
+                                uint32_t* adj, hipStream_t s);
 }  // namespace ngt_amd

@@ -75,4 +75,20 @@ hipError_t launch_prepare_queries(const float* d_in, uint32_t dim, uint32_t nq, 
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) pad_adjacency_kernel(const uint64_t* off, const uint32_t* edges,
+                                                            uint64_t nrows, uint64_t stride, uint32_t* adj) {
+  const uint64_t total = nrows * stride;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t v = i / stride, e = i - v * stride;
+    const uint64_t b = off[v], n = off[v + 1] - b;
+    adj[i] = e < n ? edges[b + e] : 0u;
+  }
+}
+
+hipError_t launch_pad_adjacency(const uint64_t* off, const uint32_t* edges, uint64_t nrows, uint64_t stride,
+                                uint32_t* adj, hipStream_t s) {
+  hipLaunchKernelGGL(pad_adjacency_kernel, dim3(8192), dim3(256), 0, s, off, edges, nrows, stride, adj);
+  return hipGetLastError();
+}
+
 }  // namespace ngt_amd

@@ -23,6 +23,7 @@
 // so the traversal is the reference's, not an approximation of it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ngt_device.h"
 #include "ngt_kernels.h"
@@ -174,13 +175,22 @@ __device__ __forceinline__ uint32_t ht_hash(uint32_t id, uint32_t shift) {
   return (id * 0x9E3779B1u) >> shift;
 }
 
-// Insert `id` into the visited set; true if it was not present.
+// Insert `id` into the visited set; true if it was not present.  Two exact
+// forms: an LDS open-addressing hash (small searches), or the slot's HBM
+// byte array of query epochs (vis[id] == epoch <=> visited).  The byte form
+// needs no read-modify-write: the test is a plain L2 load (sc1, so this CU's
+// L1 cannot serve a stale line) and the mark is a plain byte store -- no
+// scattered device atomics (MI355X_MICROARCH.md, Global float atomics: 64 lanes
+// in 64 rows run ~17x slower than contiguous).
 __device__ __forceinline__ bool visit(const SearchArgs& a, SearchState& st, uint32_t id,
-                                      bool bitmap_mode, uint32_t* bitmap) {
-  if (bitmap_mode) {
-    const uint32_t bit = 1u << (id & 31);
-    const uint32_t old = atomicOr(bitmap + (id >> 5), bit);
-    return !(old & bit);
+                                      bool vis_mode, uint8_t* vis, uint32_t epoch) {
+  if (vis_mode) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
+    const uint32_t word = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = (word >> (8 * (id & 3))) & 0xffu;
+    if (old == epoch) return false;
+    vis[id] = (uint8_t)epoch;
+    return true;
   }
   const uint32_t mask = (1u << a.ht_log2) - 1;
   uint32_t h = ht_hash(id, 32 - a.ht_log2);
@@ -192,12 +202,12 @@ __device__ __forceinline__ bool visit(const SearchArgs& a, SearchState& st, uint
   }
 }
 
-// Move the LDS hash contents into the per-slot HBM bitmap (exact overflow path).
-__device__ void ht_to_bitmap(const SearchArgs& a, SearchState& st, uint32_t* bitmap) {
+// Move the LDS hash contents into the slot's epoch array (exact overflow path).
+__device__ void ht_to_vis(const SearchArgs& a, SearchState& st, uint8_t* vis, uint32_t epoch) {
   const uint32_t n = 1u << a.ht_log2;
   for (uint32_t i = lane_id(); i < n; i += 64) {
     const uint32_t id = st.ht[i];
-    if (id) atomicOr(bitmap + (id >> 5), 1u << (id & 31));
+    if (id) vis[id] = (uint8_t)epoch;
   }
   __threadfence_block();
 }
@@ -243,14 +253,76 @@ __device__ __forceinline__ uint32_t compact(uint64_t* v, uint32_t n, float expr)
   return out;
 }
 
-template <int M, typename T>
-__global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
+// L2 over float rows with a compile-time chunk count (dp = 16 * NCH): the
+// query lives in registers and the loads of two 16-row groups (32 rows,
+// 16 KiB at dp = 128) are all issued before the first FMA, so one batch costs
+// one memory round trip.  Same quad mapping and folds as dist_f32<kL2>, hence
+// bit-identical results.  Out-of-range lanes read the dummy row 0.
+template <int NCH>
+__device__ __forceinline__ float l2_fold_rows(const float4* qq, const float4 (&v)[NCH]) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NCH; i++) {
+    const float4 q = qq[4 * i];  // query stays in LDS: ds_read_b128, saves 4*NCH VGPRs
+    const float vx = q.x - v[i].x, vy = q.y - v[i].y, vz = q.z - v[i].z, vw = q.w - v[i].w;
+    acc.x = __builtin_fmaf(vx, vx, acc.x);
+    acc.y = __builtin_fmaf(vy, vy, acc.y);
+    acc.z = __builtin_fmaf(vz, vz, acc.z);
+    acc.w = __builtin_fmaf(vw, vw, acc.w);
+  }
+  return (float)sqrt((double)fold16(acc));
+}
+
+// G = 16-row groups whose loads are in flight together (G=1: 16 rows / 8 KiB
+// per round trip at dp=128, low VGPR count, more resident waves; G=2: 32 rows).
+template <int NCH, int G>
+__device__ __forceinline__ void eval_l2f_fast(const float* qlds, const uint8_t* rows, uint64_t row_bytes,
+                                              const uint32_t* ids, float* dists, int m) {
+  const int lane = lane_id();
+  const int g = lane & 3, rs = lane >> 2;
+  const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
+  for (int r0 = 0; r0 < m; r0 += 16 * G) {
+    float4 v[G][NCH];
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+      if (j == 0 || r0 + 16 * j < m) {
+        const int r = r0 + 16 * j + rs;
+        const uint32_t id = r < m ? ids[r] : 0u;
+        const float4* x = reinterpret_cast<const float4*>(rows + (uint64_t)id * row_bytes) + g;
+#pragma unroll
+        for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+      if (j == 0 || r0 + 16 * j < m) {
+        const int r = r0 + 16 * j + rs;
+        const float d = l2_fold_rows<NCH>(qq, v[j]);
+        if (g == 0 && r < m) dists[r] = d;
+      }
+    }
+  }
+}
+
+template <int M, typename T, int NCH, int G>
+__device__ __forceinline__ void eval_any(const T* qlds, const SearchArgs& a, const uint32_t* ids, float* dists,
+                                         int m) {
+  if constexpr (NCH > 0 && M == kL2 && sizeof(T) == 4) {
+    eval_l2f_fast<NCH, G>(reinterpret_cast<const float*>(qlds), a.rows, a.row_bytes, ids, dists, m);
+  } else {
+    eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, ids, dists, m);
+  }
+}
+
+template <int M, typename T, int NCH, int G>
+__global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = lane_id();
   SearchState st;
   uint8_t* p = smem;
+  const bool use_hash = a.ht_log2 != 0;
   st.ht = reinterpret_cast<uint32_t*>(p);
-  p += (size_t)4 << a.ht_log2;
+  if (use_hash) p += (size_t)4 << a.ht_log2;
   st.cq = reinterpret_cast<uint64_t*>(p);
   p += (size_t)8 * a.cq_cap;
   st.res = reinterpret_cast<uint64_t*>(p);
@@ -262,9 +334,9 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
   T* qlds = reinterpret_cast<T*>(p);
 
   const uint32_t slot = blockIdx.x;
-  uint32_t* bitmap = a.bitmap + (uint64_t)slot * a.bitmap_words;
+  uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
   uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
-  const uint32_t hcap = 1u << a.ht_log2;
+  const uint32_t hcap = use_hash ? 1u << a.ht_log2 : 0u;
   const uint32_t hlimit = hcap - (hcap >> 2);  // 75 % load factor
 
   for (;;) {
@@ -276,11 +348,19 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
     // ---- per-query init -----------------------------------------------
     for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
     load_query<T>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
+    // next epoch of this slot's visited bytes; wipe the array every 255 queries
+    uint32_t epoch = a.slot_epoch[slot] + 1;
+    if (epoch > 255) {
+      uint4* v4 = reinterpret_cast<uint4*>(vis);
+      for (uint64_t i = lane; i < a.vis_stride / 16; i += 64) v4[i] = make_uint4(0, 0, 0, 0);
+      epoch = 1;
+    }
     __syncthreads();
+    if (lane == 0) a.slot_epoch[slot] = epoch;
 
-    bool bitmap_mode = false;
+    bool bitmap_mode = !use_hash;
     uint32_t nvisited = 0;
-    uint32_t ncq = 0, nspill = 0, nres = 0;
+    uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0;
     float radius = a.radius;
     const uint32_t k = a.k;
@@ -292,12 +372,12 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
       const uint32_t m = ns - base < 64 ? ns - base : 64;
       if ((uint32_t)lane < m) st.nid[lane] = a.seeds[sb + base + lane];
       __syncthreads();
-      eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, st.nid, st.nd, (int)m);
+      eval_any<M, T, NCH, G>(qlds, a, st.nid, st.nd, (int)m);
       __syncthreads();
       if ((uint32_t)lane < m) {
         const uint32_t id = st.nid[lane];
         const uint64_t key = make_key(st.nd[lane], id);
-        visit(a, st, id, bitmap_mode, bitmap);
+        visit(a, st, id, bitmap_mode, vis, epoch);
         if (ncq + lane < a.cq_cap) st.cq[ncq + lane] = key;
         else spill[nspill + (ncq + lane - a.cq_cap)] = key;
       }
@@ -307,18 +387,17 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
         const float d = st.nd[j];
         if (d <= a.radius) res_insert(st.res, nres, k, make_key(d, st.nid[j]));
       }
-      const uint32_t add = m;
-      if (ncq + add <= a.cq_cap) {
-        ncq += add;
+      if (ncq + m <= a.cq_cap) {
+        ncq += m;
       } else {
-        nspill += ncq + add - a.cq_cap;
+        nspill += ncq + m - a.cq_cap;
         ncq = a.cq_cap;
       }
       ndist += m;
       nvisited += m;
       __syncthreads();
       if (!bitmap_mode && nvisited > hlimit) {
-        ht_to_bitmap(a, st, bitmap);
+        ht_to_vis(a, st, vis, epoch);
         bitmap_mode = true;
         __syncthreads();
       }
@@ -341,10 +420,10 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
       }
       const uint64_t wbest = wave_min_u64(best);
       if (wbest == ~0ull) break;
+      if (key_dist(wbest) > expr) break;
       const uint64_t owner = ballot64(best == wbest);
       const int olane = __ffsll((long long)owner) - 1;
       bidx = __shfl(bidx, olane, 64);
-      if (key_dist(wbest) > expr) break;
       if (lane == 0) {
         if (bidx & 0x80000000u) spill[bidx & 0x7fffffffu] = spill[nspill - 1];
         else st.cq[bidx] = st.cq[ncq - 1];
@@ -354,71 +433,78 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
       nexp++;
 
       const uint32_t target = key_id(wbest);
-      const uint64_t eb = a.edge_off[target];
-      uint64_t deg = a.edge_off[target + 1] - eb;
-      if (deg > a.edge_size) deg = a.edge_size;
-      nedge += deg;
+      // adjacency: padded fixed-stride rows (one load, 0-terminated) or CSR
+      uint64_t eb, deg;
+      const bool padded = a.adj != nullptr;
+      if (padded) {
+        eb = (uint64_t)target * a.adj_stride;
+        deg = a.adj_stride < a.edge_size ? a.adj_stride : a.edge_size;
+      } else {
+        eb = a.edge_off[target];
+        deg = a.edge_off[target + 1] - eb;
+        if (deg > a.edge_size) deg = a.edge_size;
+      }
 
       for (uint64_t base = 0; base < deg; base += 64) {
         const uint32_t cnt = (uint32_t)(deg - base < 64 ? deg - base : 64);
-        bool fresh = false;
         uint32_t id = 0;
-        if ((uint32_t)lane < cnt) {
-          id = a.edges[eb + base + lane];
-          fresh = visit(a, st, id, bitmap_mode, bitmap);
-        }
+        if ((uint32_t)lane < cnt) id = padded ? a.adj[eb + base + lane] : a.edges[eb + base + lane];
+        const uint64_t vmask = ballot64(id != 0u);
+        nedge += (uint64_t)__popcll(vmask);
+        const bool fresh = id != 0u && visit(a, st, id, bitmap_mode, vis, epoch);
         const uint64_t fmask = ballot64(fresh);
         const uint32_t m = (uint32_t)__popcll(fmask);
         if (fresh) st.nid[mbcnt(fmask)] = id;
         nvisited += m;
         __syncthreads();
-        if (m == 0) continue;
-        eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, st.nid, st.nd, (int)m);
-        __syncthreads();
-        ndist += m;
-        nvisit += m;
-        // accept in neighbour order (Graph.cpp:471-483); only candidates
-        // within the radius at batch start can be accepted.
-        uint64_t okmask = ballot64((uint32_t)lane < m && st.nd[lane] <= expr);
-        while (okmask) {
-          const int j = __ffsll((long long)okmask) - 1;
-          okmask &= okmask - 1;
-          const float d = st.nd[j];
-          if (!(d <= expr)) continue;
-          const uint64_t key = make_key(d, st.nid[j]);
-          if (ncq >= a.cq_cap) {
-            ncq = compact(st.cq, ncq, expr);
-            if (nspill) {
-              nspill = compact(spill, nspill, expr);
-            }
-          }
-          if (ncq < a.cq_cap) {
-            if (lane == 0) st.cq[ncq] = key;
-            ncq++;
-          } else {
-            if (nspill >= a.spill_cap) {
-              if (lane == 0) atomicOr(a.error, 1);
-            } else {
-              if (lane == 0) spill[nspill] = key;
-              nspill++;
-            }
-          }
-          if (d <= radius) {
-            res_insert(st.res, nres, k, key);
-            if (nres >= k) {
-              radius = key_dist(st.res[k - 1]);
-              expr = __fmul_rn(a.coef, radius);
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-        __syncthreads();
-        // exact overflow of the visited set into the HBM bitmap
-        if (!bitmap_mode && nvisited > hlimit) {
-          ht_to_bitmap(a, st, bitmap);
-          bitmap_mode = true;
+        if (m != 0) {
+          eval_any<M, T, NCH, G>(qlds, a, st.nid, st.nd, (int)m);
           __syncthreads();
+          ndist += m;
+          nvisit += m;
+          // accept in neighbour order (Graph.cpp:471-483); only candidates
+          // within the radius at batch start can be accepted.
+          uint64_t okmask = ballot64((uint32_t)lane < m && st.nd[lane] <= expr);
+          while (okmask) {
+            const int j = __ffsll((long long)okmask) - 1;
+            okmask &= okmask - 1;
+            const float d = st.nd[j];
+            if (!(d <= expr)) continue;
+            const uint64_t key = make_key(d, st.nid[j]);
+            if (ncq >= a.cq_cap) {
+              ncq = compact(st.cq, ncq, expr);
+              if (nspill) nspill = compact(spill, nspill, expr);
+            }
+            if (ncq < a.cq_cap) {
+              if (lane == 0) st.cq[ncq] = key;
+              ncq++;
+            } else {
+              if (nspill >= a.spill_cap) {
+                if (lane == 0) atomicOr(a.error, 1);
+              } else {
+                if (lane == 0) spill[nspill] = key;
+                nspill++;
+              }
+            }
+            if (d <= radius) {
+              res_insert(st.res, nres, k, key);
+              if (nres >= k) {
+                radius = key_dist(st.res[k - 1]);
+                expr = __fmul_rn(a.coef, radius);
+              }
+            }
+            __builtin_amdgcn_wave_barrier();
+          }
+          if (ncq + nspill > maxq) maxq = ncq + nspill;
+          __syncthreads();
+          // exact overflow of the visited set into the HBM bitmap
+          if (!bitmap_mode && nvisited > hlimit) {
+            ht_to_vis(a, st, vis, epoch);
+            bitmap_mode = true;
+            __syncthreads();
+          }
         }
+        if (padded && vmask != ~0ull) break;  // 0-terminated list ended in this chunk
       }
     }
 
@@ -434,19 +520,12 @@ __global__ void __launch_bounds__(64) ngt_graph_search_kernel(SearchArgs a) {
         c[0] = ndist;
         c[1] = nvisit;
         c[2] = nexp;
-        c[3] = bitmap_mode ? 1 : 0;
+        c[3] = (bitmap_mode && use_hash) ? 1 : 0;
         c[4] = nedge;
-        c[5] = 0;
+        c[5] = maxq;
         c[6] = 0;
         c[7] = 0;
       }
-    }
-    if (bitmap_mode) {
-      // leave the slot's bitmap clean for the next query
-      uint4* bm = reinterpret_cast<uint4*>(bitmap);
-      const uint64_t n16 = a.bitmap_words / 4;
-      for (uint64_t i = lane; i < n16; i += 64) bm[i] = make_uint4(0, 0, 0, 0);
-      __threadfence_block();
     }
     __syncthreads();
   }
@@ -590,7 +669,7 @@ hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipSt
 }
 
 size_t search_lds_bytes(const SearchArgs& a, int otype) {
-  size_t b = ((size_t)4 << a.ht_log2) + (size_t)8 * a.cq_cap;
+  size_t b = (a.ht_log2 ? ((size_t)4 << a.ht_log2) : 0) + (size_t)8 * a.cq_cap;
   b += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   b += 512;
   b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
@@ -601,7 +680,20 @@ hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint3
                                hipStream_t s) {
   if (a.nq == 0) return hipSuccess;
   const size_t lds = search_lds_bytes(a, otype);
-#define L_SEARCH(MM, TT) hipLaunchKernelGGL((ngt_graph_search_kernel<MM, TT>), dim3(slots), dim3(64), lds, s, a)
+  static int groups = [] {
+    const char* v = getenv("NGT_AMD_GROUPS");
+    return v ? atoi(v) : 1;
+  }();
+  if (metric == kL2 && otype == kFloat && (a.dp == 128 || a.dp == 96)) {
+    if (a.dp == 128 && groups == 2)
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 8, 2>), dim3(slots), dim3(64), lds, s, a);
+    else if (a.dp == 128)
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 8, 1>), dim3(slots), dim3(64), lds, s, a);
+    else
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 6, 1>), dim3(slots), dim3(64), lds, s, a);
+    return hipGetLastError();
+  }
+#define L_SEARCH(MM, TT) hipLaunchKernelGGL((ngt_graph_search_kernel<MM, TT, 0, 1>), dim3(slots), dim3(64), lds, s, a)
   NGT_DISPATCH(metric, otype, L_SEARCH);
 #undef L_SEARCH
   return hipGetLastError();

@@ -223,11 +223,16 @@ def _random_graph(n, dim, deg, seed):
     return rows, offs, e.reshape(-1)
 
 
-@pytest.mark.parametrize("ht,cq", [("12", "1024"), ("8", "64"), ("9", "128")])
-def test_overflow_paths_exact(monkeypatch, ht, cq):
-    monkeypatch.setenv("NGT_AMD_HT_LOG2", ht)
+@pytest.mark.parametrize("ht,cq,adj", [("12", "1024", "1"), ("8", "64", "1"), ("9", "128", "0"),
+                                       ("bitmap", "1024", "1"), ("bitmap", "64", "0")])
+@pytest.mark.parametrize("dim", [32, 128])
+def test_overflow_paths_exact(monkeypatch, ht, cq, adj, dim):
+    if ht != "bitmap":
+        monkeypatch.setenv("NGT_AMD_HT_LOG2", ht)
     monkeypatch.setenv("NGT_AMD_CQ_CAP", cq)
-    n, dim, deg = 3000, 32, 24
+    monkeypatch.setenv("NGT_AMD_ADJ", adj)
+    vh = -1 if ht == "bitmap" else 0
+    n, deg = 3000, 24
     rows, offs, edges = _random_graph(n, dim, deg, 11)
     ix = DeviceIndex("l2", "float", dim)
     ix.set_objects(rows)
@@ -235,8 +240,9 @@ def test_overflow_paths_exact(monkeypatch, ht, cq):
     rng = np.random.default_rng(3)
     qs = rng.random((24, dim), dtype=np.float32)
     seeds = [rng.choice(np.arange(1, n), 10, replace=False).astype(np.uint32) for _ in range(24)]
-    for eps in [0.0, 0.3, 1.0]:
-        gi, gd, gn, cnt = ix.search(qs, k=20, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN, seeds=seeds)
+    for eps in [0.0, 0.3, 1.0]:  # noqa: B007
+        gi, gd, gn, cnt = ix.search(qs, k=20, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN, seeds=seeds,
+                                    visited_hash_log2=vh)
         for i in range(24):
             oid, od, ocnt = O.search("l2", rows, offs, edges, qs[i], seeds[i], 20, np.float32(eps))
             assert list(gi[i, :gn[i]]) == list(oid), (eps, i)
