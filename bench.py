@@ -160,10 +160,10 @@ def main():
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--target", type=float, default=0.95)
-    ap.add_argument("--knn", type=int, default=64)
-    ap.add_argument("--out-deg", type=int, default=16)
-    ap.add_argument("--in-deg", type=int, default=40)
-    ap.add_argument("--max-deg", type=int, default=64)
+    ap.add_argument("--knn", type=int, default=128)
+    ap.add_argument("--out-deg", type=int, default=48)
+    ap.add_argument("--in-deg", type=int, default=96)
+    ap.add_argument("--max-deg", type=int, default=160)
     ap.add_argument("--seed-size", type=int, default=10)
     ap.add_argument("--eps", type=str, default="")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -230,22 +230,37 @@ def main():
                          d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=stream,
                          visited_hash_log2=args.visited)
 
-    # epsilon sweep (ngt eval semantics: mean recall@k over the queries)
-    cands = [float(x) for x in args.eps.split(",")] if args.eps else \
-        [0.0, 0.02, 0.04, 0.06, 0.08, 0.1, 0.12, 0.15, 0.18, 0.22, 0.26, 0.3, 0.35, 0.4, 0.5, 0.6, 0.8]
-    chosen, rec = None, 0.0
+    # epsilon search (ngt eval semantics: mean recall@k over the queries):
+    # the smallest epsilon whose recall@k reaches the target, by bisection
     sweep = []
-    for eps in cands:
+
+    def measure(eps):
         run(eps)
         torch.cuda.synchronize()
-        rec = recall_at(out_i.cpu().numpy(), gt, K)
-        sweep.append((eps, rec, ix.last_search_kernel_ms()))
-        log("eps %.3f recall@%d %.4f kernel %.2f ms" % (eps, K, rec, sweep[-1][2]))
-        if rec >= args.target:
-            chosen = eps
-            break
-    if chosen is None:
+        r = recall_at(out_i.cpu().numpy(), gt, K)
+        sweep.append((round(eps, 5), r, ix.last_search_kernel_ms()))
+        log("eps %.4f recall@%d %.4f kernel %.2f ms" % (eps, K, r, sweep[-1][2]))
+        return r
+
+    if args.eps:
+        cands = [float(x) for x in args.eps.split(",")]
         chosen = cands[-1]
+        for eps in cands:
+            if measure(eps) >= args.target:
+                chosen = eps
+                break
+    else:
+        lo, hi = 0.0, 0.05
+        while measure(hi) < args.target and hi < 2.0:
+            lo, hi = hi, hi * 2
+        while hi - lo > 0.002:
+            mid = 0.5 * (lo + hi)
+            if measure(mid) >= args.target:
+                hi = mid
+            else:
+                lo = mid
+        chosen = hi
+    rec = measure(chosen)
     if dist is not None:
         # all ranks use the largest epsilon any rank needed
         t = torch.tensor([chosen], device=dev)
@@ -286,6 +301,10 @@ def main():
     # B(q) = U(q)*Dp*4 + E(q)*4 + Dp*4 + k*8   
     c = cnt.cpu().numpy().astype(np.float64)
     U, E = c[:, 0].sum(), c[:, 4].sum()
+    if "stamps" in os.environ.get("NGT_AMD_LIB", ""):
+        tot = c[:, [5, 6, 7, 3]].mean(0)
+        log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
+            tot[0], tot[1], tot[2], tot[3], tot.sum()))
     alg_bytes = U * dp * 4 + E * 4 + NQ * (dp * 4 + K * 8)
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9

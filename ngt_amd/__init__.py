@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libngt_amd.so")
+LIB_PATH = os.environ.get("NGT_AMD_LIB") or os.path.join(HERE, "libngt_amd.so")
 _LIB = None
 
 

@@ -30,6 +30,27 @@
 
 namespace ngt_amd {
 
+// Diagnostic build only (-DNGT_AMD_STAMPS, libngt_amd_stamps.so): per-query
+// shader-clock totals of the search phases land in counters [5..7]; the
+// product build compiles these to nothing.
+#ifdef NGT_AMD_STAMPS
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define NGT_MARK(dst)              \
+  do {                             \
+    const uint64_t now_ = stamp(); \
+    dst += now_ - t_last;          \
+    t_last = now_;                 \
+  } while (0)
+#else
+#define NGT_MARK(dst)
+#endif
+
 // ---------------------------------------------------------------------------
 // glibc random(3) TYPE_3, for srand(leafID) (lib/NGT/Index.h:1555-1559).
 // ---------------------------------------------------------------------------
@@ -362,6 +383,11 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
     uint32_t nvisited = 0;
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0;
+    uint64_t t_pop = 0, t_adj = 0, t_eval = 0, t_last = 0, t_rest = 0;
+    (void)t_pop; (void)t_adj; (void)t_eval; (void)t_last; (void)t_rest;
+#ifdef NGT_AMD_STAMPS
+    t_last = stamp();
+#endif
     float radius = a.radius;
     const uint32_t k = a.k;
 
@@ -407,6 +433,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
 
     // ---- best-first loop (Graph.cpp:430-486) ----------------------------
     for (;;) {
+      NGT_MARK(t_rest);
       // pop the minimum key
       uint64_t best = ~0ull;
       uint32_t bidx = 0xffffffffu;
@@ -431,6 +458,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
       if (bidx & 0x80000000u) nspill--; else ncq--;
       __syncthreads();
       nexp++;
+      NGT_MARK(t_pop);
 
       const uint32_t target = key_id(wbest);
       // adjacency: padded fixed-stride rows (one load, 0-terminated) or CSR
@@ -457,9 +485,11 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
         if (fresh) st.nid[mbcnt(fmask)] = id;
         nvisited += m;
         __syncthreads();
+        NGT_MARK(t_adj);
         if (m != 0) {
           eval_any<M, T, NCH, G>(qlds, a, st.nid, st.nd, (int)m);
           __syncthreads();
+          NGT_MARK(t_eval);
           ndist += m;
           nvisit += m;
           // accept in neighbour order (Graph.cpp:471-483); only candidates
@@ -522,9 +552,16 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
         c[2] = nexp;
         c[3] = (bitmap_mode && use_hash) ? 1 : 0;
         c[4] = nedge;
+#ifdef NGT_AMD_STAMPS
+        c[5] = t_pop;
+        c[6] = t_adj;
+        c[7] = t_eval;
+        c[3] = t_rest;  // accept + loop overhead
+#else
         c[5] = maxq;
         c[6] = 0;
         c[7] = 0;
+#endif
       }
     }
     __syncthreads();
