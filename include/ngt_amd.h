@@ -27,7 +27,8 @@
  * Conventions: plain pointers and sizes; functions return 0 on success and a
  * negative value on failure with a message retrievable by
  * ngt_amd_last_error().  `*_device` variants take device pointers and enqueue
- * on the given HIP stream (hipStream_t passed as void*); the others take host
+ * on the given HIP stream (hipStream_t passed as void*; NULL = the default
+ * stream, ordered with every blocking stream); the others take host
  * pointers and are synchronous.  There is no CPU fallback: without a usable
  * gfx950 device every compute call fails with an error.
  */

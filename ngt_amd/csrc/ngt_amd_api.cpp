@@ -150,7 +150,7 @@ extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distanc
   ix->row_bytes = (uint64_t)ix->dp * ix->esize;
   ix->cu_count = prop.multiProcessorCount;
   ix->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
-  if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
+  if (hipStreamCreateWithFlags(&ix->stream, hipStreamDefault) != hipSuccess ||
       hipEventCreate(&ix->ev0) != hipSuccess || hipEventCreate(&ix->ev1) != hipSuccess) {
     delete ix;
     return fail("ngt_amd_index_create: stream/event creation failed");
@@ -312,7 +312,7 @@ extern "C" uint64_t ngt_amd_resolve_edge_size(const ngt_amd_index* ix, int64_t e
   return 0;  // invalid -> caller reports
 }
 
-static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a) {
+static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a, hipStream_t s) {
   size_t lds = search_lds_bytes(a, ix->otype);
   if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
@@ -324,9 +324,10 @@ static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a) {
   uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * ix->cu_count, std::max<uint64_t>(max_slots, 64));
   if (slots != ix->slots || stride != ix->vis_stride || !ix->spill.p) {
     HIP_OK(ix->vis.alloc((size_t)slots * stride));
-    HIP_OK(hipMemset(ix->vis.p, 0, (size_t)slots * stride));
+    // zeroed on the launch stream so the first search is ordered after it
+    HIP_OK(hipMemsetAsync(ix->vis.p, 0, (size_t)slots * stride, s));
     HIP_OK(ix->slot_epoch.alloc(slots));
-    HIP_OK(hipMemset(ix->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t)));
+    HIP_OK(hipMemsetAsync(ix->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t), s));
     HIP_OK(ix->spill.alloc((size_t)slots * ix->spill_cap));
     ix->slots = slots;
     ix->vis_stride = stride;
@@ -409,7 +410,7 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
     a.seeds = d_seeds;
     a.seed_off = d_seed_off;
   }
-  if (ensure_scratch(ix, a)) return -1;
+  if (ensure_scratch(ix, a, s)) return -1;
   a.vis = ix->vis.p;
   a.vis_stride = ix->vis_stride;
   a.slot_epoch = ix->slot_epoch.p;
@@ -457,7 +458,7 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
   if (!ix || !prm || (!d_queries && nq)) return fail("ngt_amd_search_device: bad arguments");
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+  hipStream_t s = (hipStream_t)stream;  // null = the default stream
   if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
     std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
@@ -492,7 +493,7 @@ extern "C" int ngt_amd_prepare_queries_device(ngt_amd_index* ix, const float* d_
                                               void* d_out, void* stream) {
   if (!ix || (!d_in && nq) || (!d_out && nq)) return fail("ngt_amd_prepare_queries_device: bad arguments");
   if (nq == 0) return 0;
-  hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+  hipStream_t s = (hipStream_t)stream;  // null = the default stream
   bool normalize = ix->metric == 5 || ix->metric == 6 || ix->metric == 9;
   HIP_OK(launch_prepare_queries(d_in, ix->dim, nq, ix->dp, ix->otype, normalize, d_out, ix->error.p, s));
   return 0;
@@ -551,7 +552,7 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
   if (!ix || (!d_queries && nq) || k == 0) return fail("ngt_amd_linear_search_device: bad arguments");
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+  hipStream_t s = (hipStream_t)stream;  // null = the default stream
   // enough slices to fill the chip: ~4 waves per CU over all queries
   uint64_t want = ((uint64_t)ix->cu_count * 16 + nq - 1) / nq;
   uint64_t maxs = (ix->nrows + 255) / 256;

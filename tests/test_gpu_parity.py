@@ -274,3 +274,46 @@ def test_edge_cases():
                               edge_size=3)
         assert list(gi[i, :gn[i]]) == list(oid)
     ix.close()
+
+
+def test_device_api_first_launch_exact():
+    """The *_device entry points on the default (NULL) stream: the very first
+    launch (which allocates and zeroes the per-slot visited arrays) must already
+    be exact, and repeated launches must agree bit for bit."""
+    import torch
+    n, dim, deg, nq = 60000, 32, 24, 256
+    rows, offs, edges = _random_graph(n, dim, deg, 21)
+    dev = torch.device("cuda:0")
+    d_rows = torch.from_numpy(rows).to(dev)
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_edges = torch.from_numpy(edges.astype(np.int32)).to(dev)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects_device(d_rows.data_ptr(), n)
+    ix.set_graph_device(d_offs.data_ptr(), d_edges.data_ptr(), len(edges))
+    rng = np.random.default_rng(8)
+    qs = rng.random((nq, dim), dtype=np.float32)
+    seeds = np.stack([rng.choice(np.arange(1, n), 10, replace=False) for _ in range(nq)]).astype(np.uint32)
+    d_q = torch.from_numpy(qs).to(dev)
+    d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+    d_soff = torch.arange(0, nq + 1, dtype=torch.int64, device=dev) * 10
+    outs = []
+    for _ in range(3):
+        oi = torch.zeros((nq, 10), dtype=torch.int32, device=dev)
+        od = torch.zeros((nq, 10), dtype=torch.float32, device=dev)
+        on = torch.zeros((nq,), dtype=torch.int32, device=dev)
+        cnt = torch.zeros((nq, 8), dtype=torch.int64, device=dev)
+        ix.search_device(d_q.data_ptr(), dim * 4, nq, oi.data_ptr(), od.data_ptr(), on.data_ptr(), cnt.data_ptr(),
+                         k=10, epsilon=0.3, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                         d_seed_off=d_soff.data_ptr(), stream=None, visited_hash_log2=-1)
+        torch.cuda.synchronize()
+        outs.append((oi.cpu().numpy().view(np.uint32), od.cpu().numpy(), on.cpu().numpy(), cnt.cpu().numpy()))
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1].view(np.uint32), outs[0][1].view(np.uint32))
+        assert np.array_equal(o[3][:, :3], outs[0][3][:, :3])
+    gi, gd, gn, cnt = outs[0]
+    for i in range(0, nq, 4):
+        oid, od_, ocnt = O.search("l2", rows, offs, edges, qs[i], seeds[i], 10, np.float32(0.3))
+        assert list(gi[i, :gn[i]]) == list(oid), i
+        assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od_.view(np.uint32))
+        assert int(cnt[i, 0]) == int(ocnt[0])
+    ix.close()
