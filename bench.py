@@ -308,10 +308,7 @@ def main():
     alg_bytes = U * dp * 4 + E * 4 + NQ * (dp * 4 + K * 8)
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    tf = os.environ.get("NGT_BENCH_TRAFFIC_BYTES")
-    if tf:
-        traffic = float(tf)
+    traffic = measured_traffic("kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg), chosen)
 
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
@@ -350,6 +347,24 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def measured_traffic(graph, eps):
+    """HBM bytes per launch of the search kernel from the committed PMC passes
+    (profiles/traffic.json, written from rocprofv3 FETCH_SIZE/WRITE_SIZE) for this
+    exact graph and epsilon; NGT_BENCH_TRAFFIC_BYTES overrides; else None."""
+    tf = os.environ.get("NGT_BENCH_TRAFFIC_BYTES")
+    if tf:
+        return float(tf)
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")) as f:
+            entries = json.load(f)["entries"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for e in entries:
+        if e["graph"] == graph and abs(e["epsilon"] - eps) < 1e-7:
+            return float(e["traffic_bytes"])
+    return None
 
 
 def cpu_baseline(rows, offsets, edges, qry, seeds, eps, K, dp, budget_s):

@@ -33,6 +33,14 @@ def lib():
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise NativeError("%s is missing: run ngt_amd.build() (or `make -C ngt_amd`)" % LIB_PATH)
+        # One HIP runtime per process: torch bundles its own libamdhip64 (found
+        # by file name, not SONAME).  Loading torch first lets our library bind
+        # to that same runtime (SONAME libamdhip64.so.7); loading ours first would
+        # leave torch a second runtime that cannot see the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _LIB = ctypes.CDLL(LIB_PATH)
         from . import _sigs
         _sigs.declare(_LIB)
