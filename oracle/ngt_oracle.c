@@ -512,3 +512,188 @@ uint32_t ngto_tree_leaf(int metric, int otype, const void *query, size_t dp,
   if (ndist) *ndist = nd;
   return node;
 }
+
+/* ------------------------------------------------------------------------- */
+/* NGTQG: uint8 LUT, 4-bit ADC, quantized-graph search.                       */
+/* ------------------------------------------------------------------------- */
+
+void ngto_qg_lut(const float *query, const float *global, const float *local, size_t M,
+                 size_t dsub, uint8_t *lut, float *scale, float *total_offset) {
+  /* createFloatL2DistanceLookup (Quantizer.h:683-706): per subspace li and
+   * centroid k = 1..16, d = sum over the subvector of (q - g - c)^2 in float.
+   * The reference build contracts `d += sub * sub` into an FMA chain
+   * (-Ofast); pinned by tests/golden/d20_qg (dsub = 4). */
+  size_t Me = (M + 1) / 2 * 2;
+  float *d = (float *)malloc(M * 16 * sizeof(float));
+  float mn = FLT_MAX, mx = -FLT_MAX;
+  for (size_t li = 0; li < M; li++) {
+    const float *q = query + li * dsub, *g = global + li * dsub;
+    for (size_t c = 1; c <= 16; c++) {
+      const float *lc = local + (li * 17 + c) * dsub;
+      float acc = 0.0f;
+      for (size_t j = 0; j < dsub; j++) {
+        float sub = q[j] - g[j] - lc[j];
+        acc = fmaf(sub, sub, acc);
+      }
+      d[li * 16 + c - 1] = acc;
+      /* one global min/max over every subspace (:724-736) */
+      if (acc > mx) mx = acc;
+      if (acc < mn) mn = acc;
+    }
+  }
+  float offset = mn;
+  float sc = (float)((double)(mx - mn) / 255.0);  /* (:738) */
+  float tot = 0.0f;
+  for (size_t li = 0; li < M; li++) {
+    for (size_t c = 0; c < 16; c++) {
+      int32_t t = (int32_t)roundf((d[li * 16 + c] - offset) / sc);  /* (:742) */
+      lut[li * 16 + c] = (uint8_t)t;
+    }
+    tot += offset;  /* totalOffset (:749) */
+  }
+  for (size_t li = M; li < Me; li++) memset(lut + li * 16, 0, 16);  /* odd M pad (:751-757) */
+  free(d);
+  *scale = sc;
+  *total_offset = tot;
+}
+
+void ngto_qg_adc(const uint8_t *codes, size_t n, const uint8_t *lut, size_t M, float scale,
+                 float total_offset, float *out) {
+  /* Block of 16 objects = 8*Me bytes: subspace m's 16 nibbles sit at bytes
+   * [8m, 8m+8), object 2j in the low nibble of byte j, 2j+1 in the high
+   * (QuantizedObjectProcessingStream, Quantizer.h:1295-1327).  The AVX-512
+   * loop keeps two u16 accumulators per object -- even subspaces in one,
+   * odd in the other -- with saturating adds (_mm512_adds_epu16, :986-1007);
+   * unsigned saturating adds of non-negative terms equal min(sum, 65535).
+   * Epilogue: sqrt(fma(float(E + O), scale, totalOffset)) (:1020-1031; the
+   * -Ofast build contracts mul+add into vfmadd). */
+  size_t Me = (M + 1) / 2 * 2;
+  size_t nb = n == 0 ? 0 : (n - 1) / 16 + 1;
+  for (size_t b = 0; b < nb; b++) {
+    const uint8_t *blk = codes + b * 8 * Me;
+    for (size_t i = 0; i < 16 && b * 16 + i < n; i++) {
+      uint32_t e = 0, o = 0;
+      for (size_t m = 0; m < Me; m++) {
+        uint8_t byte = blk[8 * m + i / 2];
+        uint32_t code = (i & 1) ? (byte >> 4) : (byte & 15);
+        uint32_t v = lut[m * 16 + code];
+        if (m & 1) o += v; else e += v;
+      }
+      if (e > 65535) e = 65535;
+      if (o > 65535) o = 65535;
+      out[b * 16 + i] = sqrtf(fmaf((float)(e + o), scale, total_offset));
+    }
+  }
+}
+
+int ngto_qg_search(const float *rows, size_t dp, size_t nrows, const uint64_t *qoff,
+                   const uint32_t *qids, const uint64_t *code_off, const uint8_t *codes, size_t M,
+                   const uint8_t *lut, float scale, float total_offset, const float *query,
+                   const uint32_t *seeds, size_t nseeds, size_t k, float epsilon,
+                   float result_expansion, float radius, uint32_t *out_ids, float *out_dists,
+                   uint64_t *counters) {
+  /* sc.size *= resultExpansion: size_t * float -> float -> size_t (:194-196) */
+  size_t size = k;
+  if (result_expansion > 1.0f) size = (size_t)((float)size * result_expansion);
+  float coef = (float)((double)epsilon + 1.0);
+  if (coef == 0.0f) coef = (float)1.1;  /* (:207-209) */
+  uint64_t nadc = 0, nacc = 0, nexp = 0, nexact = 0;
+  if (size == 0) {
+    if (counters) counters[0] = counters[1] = counters[2] = counters[3] = 0;
+    return 0;
+  }
+  uint8_t *checked = (uint8_t *)calloc(nrows, 1);
+  heap_t unchecked = {0, 0, 0, 0}, results = {0, 0, 0, 1};
+
+  /* setupDistances with the exact L2 comparator (:214) + setupSeeds (:215) */
+  od_t *sd = (od_t *)malloc((nseeds ? nseeds : 1) * sizeof(od_t));
+  for (size_t i = 0; i < nseeds; i++) {
+    sd[i].id = seeds[i];
+    sd[i].d = ngto_distance(NGTO_L2, NGTO_FLOAT, query, rows + (size_t)seeds[i] * dp, dp);
+  }
+  nexact += nseeds;
+  qsort(sd, nseeds, sizeof(od_t), od_cmp);
+  for (size_t i = 0; i < nseeds; i++) {
+    if (results.n < size && sd[i].d <= radius) heap_push(&results, sd[i]);
+    else break;
+  }
+  if (results.n >= size) radius = results.v[0].d;
+  for (size_t i = 0; i < nseeds; i++) {
+    checked[sd[i].id] = 1;
+    heap_push(&unchecked, sd[i]);
+  }
+  free(sd);
+
+  float expr = coef * radius;  /* (:216) */
+  float *ds = NULL;
+  size_t ds_cap = 0;
+  while (unchecked.n) {
+    od_t target = heap_pop(&unchecked);
+    if (target.d > expr) break;  /* (:223-225) */
+    nexp++;
+    size_t nn = (size_t)(qoff[target.id + 1] - qoff[target.id]);
+    if (nn > ds_cap) { ds_cap = nn; ds = (float *)realloc(ds, ds_cap * sizeof(float)); }
+    ngto_qg_adc(codes + code_off[target.id], nn, lut, M, scale, total_offset, ds);  /* (:240) */
+    nadc += nn;
+    const uint32_t *nid = qids + qoff[target.id];
+    for (size_t i = 0; i < nn; i++) {  /* (:241-266) */
+      float d = ds[i];
+      if (d <= expr) {
+        if (checked[nid[i]]) continue;
+        checked[nid[i]] = 1;
+        nacc++;
+        od_t r = {nid[i], d};
+        heap_push(&unchecked, r);
+        if (d <= radius) {
+          heap_push(&results, r);
+          if (results.n >= size) {
+            if (results.n > size) heap_pop(&results);
+            radius = results.v[0].d;
+            expr = coef * radius;
+          }
+        }
+      }
+    }
+  }
+  free(ds);
+  free(unchecked.v);
+  free(checked);
+
+  size_t nres = results.n;
+  uint32_t *ids = (uint32_t *)malloc((nres ? nres : 1) * sizeof(uint32_t));
+  float *dd = (float *)malloc((nres ? nres : 1) * sizeof(float));
+  drain(&results, ids, dd);  /* moveFrom (:272) */
+  free(results.v);
+  int n;
+  if (result_expansion >= 1.0f) {
+    /* exact rerank with the index comparator, sort, resize to k (:273-299) */
+    od_t *rr = (od_t *)malloc((nres ? nres : 1) * sizeof(od_t));
+    for (size_t i = 0; i < nres; i++) {
+      rr[i].id = ids[i];
+      rr[i].d = ngto_distance(NGTO_L2, NGTO_FLOAT, query, rows + (size_t)ids[i] * dp, dp);
+    }
+    nexact += nres;
+    qsort(rr, nres, sizeof(od_t), od_cmp);
+    for (size_t i = 0; i < k; i++) {
+      out_ids[i] = i < nres ? rr[i].id : 0u;
+      out_dists[i] = i < nres ? rr[i].d : 0.0f;
+    }
+    free(rr);
+    n = (int)k;
+  } else {
+    for (size_t i = 0; i < nres; i++) {
+      out_ids[i] = ids[i];
+      out_dists[i] = dd[i];
+    }
+    n = (int)nres;
+  }
+  free(ids);
+  free(dd);
+  if (counters) {
+    counters[0] = nadc;
+    counters[1] = nacc;
+    counters[2] = nexp;
+    counters[3] = nexact;
+  }
+  return n;
+}

@@ -91,6 +91,37 @@ uint32_t ngto_tree_leaf(int metric, int otype, const void *query, size_t dp,
                         const uint32_t *in_child, const float *in_border,
                         size_t children, uint64_t *ndist);
 
+/* ---- NGTQG (quantized graph) -------------------------------------------- */
+/* QuantizedObjectDistance::createDistanceLookup(Object&, id,
+ * DistanceLookupTableUint8&) (lib/NGT/NGTQ/Quantizer.h:709-760) over
+ * createFloatL2DistanceLookup (:683-706).  query/global: D floats; local:
+ * [M][17][dsub] centroids (slot 0 unused, NGT object ids 1..16).  Writes
+ * lut[Me*16] (Me = M rounded up to even; the pad subspace is zero), the one
+ * scale and totalOffset used by the ADC. */
+void ngto_qg_lut(const float *query, const float *global, const float *local, size_t M,
+                 size_t dsub, uint8_t *lut, float *scale, float *total_offset);
+
+/* QuantizedObjectDistanceFloat::operator()(void*, float*, size_t,
+ * DistanceLookupTableUint8&) (Quantizer.h:957-1062, AVX-512 build): packed
+ * 4-bit codes of n objects (ceil(n/16) blocks of 8*Me bytes) -> out[n]. */
+void ngto_qg_adc(const uint8_t *codes, size_t n, const uint8_t *lut, size_t M, float scale,
+                 float total_offset, float *out);
+
+/* NGTQG::Index::searchQuantizedGraph (lib/NGT/NGTQ/QuantizedGraph.h:192-320)
+ * for one query, given its seeds (getSeedsFromTree / getSeedsFromGraph
+ * output, unsorted).  Quantized graph: node v has neighbours
+ * qids[qoff[v]..qoff[v+1]) and codes at codes + code_off[v].  rows: exact f32
+ * rows (padded dp) for seed distances and the rerank.  Returns the number of
+ * entries written (k when expansion >= 1: the reference's resize pads with
+ * {id 0, distance 0}); counters: [0] ADC distances, [1] accepted (visitCount
+ * semantics of this loop), [2] expansions, [3] exact distances. */
+int ngto_qg_search(const float *rows, size_t dp, size_t nrows, const uint64_t *qoff,
+                   const uint32_t *qids, const uint64_t *code_off, const uint8_t *codes, size_t M,
+                   const uint8_t *lut, float scale, float total_offset, const float *query,
+                   const uint32_t *seeds, size_t nseeds, size_t k, float epsilon,
+                   float result_expansion, float radius, uint32_t *out_ids, float *out_dists,
+                   uint64_t *counters);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@ golden-vector generator and the tests can inspect reference-built indexes:
 The product path has its own C++ loader (ngt_amd/csrc/index_io.cpp); this
 module is only used by tests/ and the golden generator.
 """
+import os
 import struct
 
 import numpy as np
@@ -181,3 +182,89 @@ def parse_search_output(text):
                 cur["ids"].append(int(parts[1]))
                 cur["dists"].append(float(parts[2]))
     return out
+
+
+# ---------------------------------------------------------------------------
+# NGTQG quantizer state (index/qg/): prf, global/obj, local-*/obj, ivt, grp
+# ---------------------------------------------------------------------------
+def read_ivt(path):
+    """qg/ivt: Repository<InvertedIndexEntry<uint16_t>> (NGTQ/Quantizer.h:105-132):
+    u64 n, then per slot '+'/'-', u32 size, u16 numOfLocalIDs, size x
+    {u32 id, u16 localID[nids] padded to 4 B}.  Returns {slot: (ids, localIDs)}."""
+    raw = open(path, "rb").read()
+    n = struct.unpack_from("<Q", raw, 0)[0]
+    off = 8
+    ents = {}
+    for slot in range(n):
+        t = raw[off:off + 1]
+        off += 1
+        if t == b"-":
+            continue
+        if t != b"+":
+            raise ValueError("corrupt ivt at slot %d" % slot)
+        sz, nids = struct.unpack_from("<IH", raw, off)
+        off += 6
+        es = 4 + ((nids * 2 - 1) // 4 + 1) * 4
+        a = np.frombuffer(raw, np.uint8, sz * es, off).reshape(sz, es)
+        off += sz * es
+        ents[slot] = (a[:, :4].copy().view(np.uint32)[:, 0], a[:, 4:4 + 2 * nids].copy().view(np.uint16))
+    if off != len(raw):
+        raise ValueError("trailing bytes in ivt")
+    return ents
+
+
+def read_qg(index_dir, graph_offs, graph_ids, max_edges=128):
+    """The quantizer state an NGTQG::Index opens (QuantizedGraph.h:170-185) and
+    the quantized graph it constructs when qg/grp is absent (:64-115)."""
+    qg = os.path.join(index_dir, "qg")
+    p = read_prf(os.path.join(qg, "prf"))
+    dim, M = int(p["Dimension"]), int(p["LocalDivisionNo"])
+    dsub = dim // M
+    g, _ = read_obj(os.path.join(qg, "global", "obj"), dim, np.float32)
+    local = np.stack([read_obj(os.path.join(qg, "local-%d" % i, "obj"), dsub, np.float32)[0][:, :dsub]
+                      for i in range(M)])
+    ents = read_ivt(os.path.join(qg, "ivt"))
+    last = max(int(ids.max()) for ids, _ in ents.values() if len(ids))
+    lid = np.zeros((last + 1, M), np.uint16)
+    for gid in sorted(ents):
+        if gid == 0:
+            continue
+        ids, l = ents[gid]
+        lid[ids] = l[:, :M]
+    n = len(graph_offs) - 1
+    me = (M + 1) // 2 * 2
+    qoff = np.zeros(n + 1, np.uint64)
+    code_off = np.zeros(n + 1, np.uint64)
+    qids, blobs = [], []
+    for v in range(n):
+        e = np.asarray(graph_ids[graph_offs[v]:graph_offs[v + 1]][:max_edges], np.uint32)
+        qids.append(e)
+        qoff[v + 1] = qoff[v] + len(e)
+        if len(e) == 0:
+            blobs.append(b"")
+            code_off[v + 1] = code_off[v]
+            continue
+        nb = (len(e) - 1) // 16 + 1
+        # stream byte blk*16*Me + 16*m + (i % 16) = localID - 1 (Quantizer.h:1295-1303)
+        lc = np.zeros((nb * 16, M), np.uint8)
+        lc[:len(e)] = lid[e] - 1
+        st = np.zeros((nb, me, 16), np.uint8)
+        st[:, :M, :] = lc.reshape(nb, 16, M).transpose(0, 2, 1)
+        st = st.reshape(-1)
+        c = (st[0::2] | (st[1::2] << 4)).astype(np.uint8).tobytes()  # compressIntoUint4 (:1305-1327)
+        blobs.append(c)
+        code_off[v + 1] = code_off[v] + len(c)
+    return {"dim": dim, "M": M, "dsub": dsub, "global": g[1].copy(), "local": local, "local_ids": lid,
+            "qoff": qoff, "qids": np.concatenate(qids) if qids else np.zeros(0, np.uint32),
+            "code_off": code_off, "codes": np.frombuffer(b"".join(blobs), np.uint8).copy()}
+
+
+def serialize_qg_grp(q):
+    """QuantizedGraphRepository::serialize (QuantizedGraph.h:117-128)."""
+    n = len(q["qoff"]) - 1
+    out = [struct.pack("<QQ", q["M"], n)]
+    for v in range(n):
+        a, b = int(q["qoff"][v]), int(q["qoff"][v + 1])
+        out.append(struct.pack("<I", b - a) + q["qids"][a:b].astype(np.uint32).tobytes())
+        out.append(q["codes"][int(q["code_off"][v]):int(q["code_off"][v + 1])].tobytes())
+    return b"".join(out)

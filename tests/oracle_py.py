@@ -132,3 +132,70 @@ def tree_seeds(metric, tree, query, k, seed_size=10, dtype=np.float32):
     seeds = np.ascontiguousarray(tree["leaf_ids"][b:e], dtype=np.uint32).copy()
     n = lib().ngto_thin_seeds(_p(seeds, ctypes.c_uint32), len(seeds), lid, seed_size, k)
     return seeds[:n].copy(), int(nd[0]), lid
+
+
+def _qg_sigs(L):
+    if getattr(L, "_qg", False):
+        return
+    vp, sz, u8p, u32p, f32p, u64p = (ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint8),
+                                     ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float),
+                                     ctypes.POINTER(ctypes.c_uint64))
+    L.ngto_qg_lut.restype = None
+    L.ngto_qg_lut.argtypes = [f32p, f32p, f32p, sz, sz, u8p, f32p, f32p]
+    L.ngto_qg_adc.restype = None
+    L.ngto_qg_adc.argtypes = [u8p, sz, u8p, sz, ctypes.c_float, ctypes.c_float, f32p]
+    L.ngto_qg_search.restype = ctypes.c_int
+    L.ngto_qg_search.argtypes = [f32p, sz, sz, u64p, u32p, u64p, u8p, sz, u8p, ctypes.c_float, ctypes.c_float,
+                                 f32p, u32p, sz, sz, ctypes.c_float, ctypes.c_float, ctypes.c_float, u32p, f32p,
+                                 u64p]
+    L._qg = True
+
+
+def qg_lut(qg, query):
+    """createDistanceLookup (NGTQ/Quantizer.h:709-760) -> (lut, scale, totalOffset)."""
+    L = lib()
+    _qg_sigs(L)
+    M = qg["M"]
+    me = (M + 1) // 2 * 2
+    q = np.ascontiguousarray(query[:qg["dim"]], dtype=np.float32)
+    g = np.ascontiguousarray(qg["global"][:qg["dim"]], dtype=np.float32)
+    loc = np.ascontiguousarray(qg["local"], dtype=np.float32)
+    lut = np.zeros(me * 16, np.uint8)
+    sc = np.zeros(1, np.float32)
+    to = np.zeros(1, np.float32)
+    L.ngto_qg_lut(_p(q, ctypes.c_float), _p(g, ctypes.c_float), _p(loc, ctypes.c_float), M, qg["dsub"],
+                  _p(lut, ctypes.c_uint8), _p(sc, ctypes.c_float), _p(to, ctypes.c_float))
+    return lut, sc[0], to[0]
+
+
+def qg_adc(qg, node, lut, scale, total):
+    L = lib()
+    _qg_sigs(L)
+    a, b = int(qg["qoff"][node]), int(qg["qoff"][node + 1])
+    codes = np.ascontiguousarray(qg["codes"][int(qg["code_off"][node]):int(qg["code_off"][node + 1])])
+    out = np.zeros(max(b - a, 1), np.float32)
+    L.ngto_qg_adc(_p(codes, ctypes.c_uint8), b - a, _p(np.ascontiguousarray(lut), ctypes.c_uint8), qg["M"],
+                  scale, total, _p(out, ctypes.c_float))
+    return out[:b - a]
+
+
+def qg_search(qg, rows, query, seeds, k, epsilon, expansion, radius=3.402823466e38):
+    """NGTQG::Index::searchQuantizedGraph (QuantizedGraph.h:192-320)."""
+    L = lib()
+    _qg_sigs(L)
+    rows = np.ascontiguousarray(rows, dtype=np.float32)
+    dp = rows.shape[1]
+    q = np.zeros(dp, np.float32)
+    q[:len(query)] = query
+    lut, sc, to = qg_lut(qg, q)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+    cap = max(k, int(k * expansion) + 1, 1)
+    ids = np.zeros(cap, np.uint32)
+    ds = np.zeros(cap, np.float32)
+    cnt = np.zeros(4, np.uint64)
+    n = L.ngto_qg_search(_p(rows, ctypes.c_float), dp, rows.shape[0], _p(qg["qoff"], ctypes.c_uint64),
+                         _p(qg["qids"], ctypes.c_uint32), _p(qg["code_off"], ctypes.c_uint64),
+                         _p(qg["codes"], ctypes.c_uint8), qg["M"], _p(lut, ctypes.c_uint8), sc, to,
+                         _p(q, ctypes.c_float), _p(seeds, ctypes.c_uint32), len(seeds), k, epsilon, expansion,
+                         radius, _p(ids, ctypes.c_uint32), _p(ds, ctypes.c_float), _p(cnt, ctypes.c_uint64))
+    return ids[:n].copy(), ds[:n].copy(), cnt
