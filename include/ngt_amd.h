@@ -159,6 +159,64 @@ int ngt_amd_prepare_queries_device(ngt_amd_index *index, const float *d_in, uint
 /* Timing of the last search call's kernels (HIP events on the search stream), ms. */
 float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
 
+/* ---- NGTQG quantized graph (L2, float objects) -------------------------- *
+ *   ngt_amd_qg_set_quantizer  <- the NGTQ::Quantizer NGTQG::Index opens from
+ *                                <index>/qg (lib/NGT/NGTQ/QuantizedGraph.h:170-185):
+ *                                global codebook centroid 1 (QG: the zero
+ *                                vector, :397-399) and the M local codebooks.
+ *   ngt_amd_qg_build_graph    <- QuantizedGraphRepository::construct (:64-115).
+ *   ngt_amd_qg_set_graph      <- QuantizedGraphRepository::deserialize (qg/grp, :130-150).
+ *   ngt_amd_qg_lut            <- QuantizedObjectDistance::createDistanceLookup
+ *                                (lib/NGT/NGTQ/Quantizer.h:709-760).
+ *   ngt_amd_qg_adc            <- QuantizedObjectDistanceFloat::operator()(void*, float*,
+ *                                size_t, DistanceLookupTableUint8&) (Quantizer.h:957-1062).
+ *   ngt_amd_qg_search[_device]<- NGTQG::Index::search(SearchQuery&) (QuantizedGraph.h:354-372):
+ *                                getSeedsFromTree + searchQuantizedGraph (:192-320).
+ * M subspaces of dsub dimensions (M * dsub = dimension), 16 centroids each;
+ * Me = M rounded up to even, at most 512. */
+typedef struct {
+  uint32_t k;               /* NGTQGQuery::size                                    */
+  float epsilon;            /* NGTQGQuery::epsilon                                 */
+  float result_expansion;   /* NGTQGQuery::result_expansion (>= 1: exact rerank)   */
+  float radius;             /* NGTQGQuery::radius; < 0 => FLT_MAX                  */
+  int32_t seed_mode;        /* NGT_AMD_SEED_TREE / _GIVEN / _RANDOM                */
+  int32_t visited_hash_log2;/* as ngt_amd_search_params                            */
+} ngt_amd_qg_search_params;
+
+/* global: [dimension] floats; local: [M][16][dsub] floats (local ids 1..16). */
+int ngt_amd_qg_set_quantizer(ngt_amd_index *index, const float *global, const float *local,
+                             uint32_t M, uint32_t dsub);
+/* local_codes: [nrows][M] bytes, localID - 1 (0..15) of every object (qg/ivt);
+ * node v keeps its first min(degree, max_edges) graph edges. */
+int ngt_amd_qg_build_graph(ngt_amd_index *index, const uint8_t *local_codes, uint32_t max_edges);
+/* Node v: neighbour ids qids[qoff[v] .. qoff[v+1]) and packed 4-bit codes
+ * codes[code_off[v] .. code_off[v+1]) in the reference stream layout. */
+int ngt_amd_qg_set_graph(ngt_amd_index *index, const uint64_t *qoff, const uint32_t *qids,
+                         const uint64_t *code_off, const uint8_t *codes);
+/* Widest quantized neighbour list (row stride of ngt_amd_qg_adc's output). */
+uint32_t ngt_amd_qg_max_degree(const ngt_amd_index *index);
+/* Per query: lut [nq][Me*16] bytes, scale [nq], total_offset [nq]. */
+int ngt_amd_qg_lut(ngt_amd_index *index, const float *queries, uint32_t nq, uint8_t *lut,
+                   float *scale, float *total_offset);
+/* ADC distances of node[i]'s whole neighbour list under query qidx[i]'s table:
+ * out [npairs][ngt_amd_qg_max_degree], out_n [npairs]. */
+int ngt_amd_qg_adc(ngt_amd_index *index, const uint8_t *lut, const float *scale,
+                   const float *total_offset, uint32_t nq, const uint32_t *qidx,
+                   const uint32_t *node, uint64_t npairs, float *out, uint32_t *out_n);
+/* Host pointers; ids/dists [nq][k], n [nq] (k when result_expansion >= 1, padded
+ * with {0, 0} as the reference's resize does), counters [nq][8] or NULL:
+ * [0] ADC distances, [1] accepted, [2] expansions, [3] exact distances,
+ * [4] 16-object code blocks read, [5] max unchecked, [6] visited spill. */
+int ngt_amd_qg_search(ngt_amd_index *index, const ngt_amd_qg_search_params *params,
+                      const float *queries, uint32_t nq, const uint32_t *seeds,
+                      const uint64_t *seed_off, uint32_t *ids, float *dists, uint32_t *n,
+                      uint64_t *counters);
+/* Device pointers; queries are prepared padded float rows, query_bytes apart. */
+int ngt_amd_qg_search_device(ngt_amd_index *index, const ngt_amd_qg_search_params *params,
+                             const void *d_queries, uint64_t query_bytes, uint32_t nq,
+                             const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,
+                             float *d_dists, uint32_t *d_n, uint64_t *d_counters, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,11 @@ class SearchParams(Structure):
                 ("visited_hash_log2", c_int32), ("reserved", c_int32)]
 
 
+class QgSearchParams(Structure):
+    _fields_ = [("k", c_uint32), ("epsilon", c_float), ("result_expansion", c_float), ("radius", c_float),
+                ("seed_mode", c_int32), ("visited_hash_log2", c_int32)]
+
+
 class ObjectDistance(Structure):
     _fields_ = [("id", c_uint), ("distance", c_float)]
 
@@ -48,6 +53,15 @@ def declare(L):
         "ngt_amd_distances": (c_int, [vp, vp, c_uint32, vp, vp, c_uint64, vp]),
         "ngt_amd_prepare_queries_device": (c_int, [vp, vp, c_uint32, vp, vp]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
+        "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),
+        "ngt_amd_qg_build_graph": (c_int, [vp, vp, c_uint32]),
+        "ngt_amd_qg_set_graph": (c_int, [vp, vp, vp, vp, vp]),
+        "ngt_amd_qg_max_degree": (c_uint32, [vp]),
+        "ngt_amd_qg_lut": (c_int, [vp, vp, c_uint32, vp, vp, vp]),
+        "ngt_amd_qg_adc": (c_int, [vp, vp, vp, vp, c_uint32, vp, vp, c_uint64, vp, vp]),
+        "ngt_amd_qg_search": (c_int, [vp, POINTER(QgSearchParams), vp, c_uint32, vp, vp, vp, vp, vp, vp]),
+        "ngt_amd_qg_search_device": (c_int, [vp, POINTER(QgSearchParams), vp, c_uint64, c_uint32, vp, vp, vp,
+                                             vp, vp, vp, vp]),
         # ---- include/NGT/Capi.h
         "ngt_open_index": (vp, [c_char_p, vp]),
         "ngt_create_graph_and_tree": (vp, [c_char_p, vp, vp]),

@@ -1,0 +1,132 @@
+// index_internal.h -- the device-resident index object behind the C ABI of
+// include/ngt_amd.h, shared by ngt_amd_api.cpp (exact path) and qg_api.cpp
+// (NGTQG path).  Not part of the public boundary.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/ngt_amd.h"
+#include "ngt_kernels.h"
+
+namespace ngt_amd {
+
+int fail(const char* fmt, ...);
+
+#define HIP_OK(expr)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return ngt_amd::fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  bool owned = true;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p && owned) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    owned = true;
+  }
+  hipError_t alloc(size_t count) {
+    if (p && owned && n >= count) return hipSuccess;
+    release();
+    n = count;
+    return hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+  }
+  hipError_t upload(const T* h, size_t count) {
+    hipError_t e = alloc(count);
+    if (e != hipSuccess) return e;
+    if (count) e = hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+  }
+};
+
+// quantized graph of an index (NGTQG), see qg_api.cpp
+struct QgState {
+  bool ready = false;
+  uint32_t M = 0, dsub = 0, Me = 0;
+  DevBuf<float> global;     // [dim]
+  DevBuf<float> local;      // [M][16][dsub]
+  DevBuf<uint32_t> qids;    // [nrows][id_stride]
+  DevBuf<uint8_t> qcodes;   // [nrows][code_stride]
+  uint32_t id_stride = 0;
+  uint64_t code_stride = 0;
+  bool has_graph = false;
+  DevBuf<uint8_t> lut;      // per-search scratch: [nq][Me*16]
+  DevBuf<float> scale, toff;
+};
+
+}  // namespace ngt_amd
+
+struct ngt_amd_index {
+  using QgState = ngt_amd::QgState;
+  template <typename T> using DevBuf = ngt_amd::DevBuf<T>;
+  int device = 0;
+  int metric = 1;
+  int otype = 2;
+  uint32_t dim = 0;
+  uint32_t dp = 0;
+  uint32_t esize = 4;
+  uint64_t row_bytes = 0;
+  uint64_t nrows = 0;
+  DevBuf<uint8_t> rows, valid;
+  std::vector<uint8_t> h_valid;
+  std::vector<uint64_t> h_degree_nonzero;  // for isEmpty in getRandomSeeds
+  DevBuf<uint64_t> edge_off;
+  DevBuf<uint32_t> edges;
+  uint64_t nedges = 0;
+  DevBuf<uint32_t> adj;          // padded fixed-stride copy of the adjacency
+  uint64_t adj_stride = 0;
+  uint64_t max_degree = 0;       // widest adjacency list
+  bool has_graph = false;
+  std::vector<uint8_t> h_graph_empty;
+  // tree
+  bool has_tree = false;
+  DevBuf<uint8_t> in_pivot;
+  DevBuf<uint32_t> in_child, leaf_ids;
+  DevBuf<float> in_border;
+  DevBuf<uint64_t> leaf_off;
+  uint32_t children = 5, root = 0;
+  // property
+  int32_t edge_size_for_search = 0;
+  int32_t dyn_base = 30, dyn_rate = 20;
+  int32_t seed_size = 10, seed_type = 0;
+  // scratch
+  DevBuf<uint32_t> work, seeds, seed_count, slot_epoch;
+  DevBuf<uint8_t> vis;
+  DevBuf<uint64_t> spill, seed_off;
+  DevBuf<int> error;
+  uint32_t slots = 0;
+  uint64_t vis_stride = 0;
+  uint32_t spill_cap = 1u << 16;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0.f;
+  int cu_count = 256;
+  size_t lds_per_cu = 160 * 1024;
+  QgState qg;                      // NGTQG quantized graph (qg_api.cpp)
+};
+
+namespace ngt_amd {
+
+constexpr uint32_t kTreeSeedStride = 128;  // max seeds per query from a tree leaf
+
+int ensure_vis_scratch(ngt_amd_index* ix, size_t lds_per_slot, hipStream_t s);
+int run_tree_seeds(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq, uint32_t k,
+                   int all_leaf_nodes, hipStream_t s);
+float coef_of(float epsilon);
+// GraphIndex::getRandomSeeds (Index.h:775-801) over the process rand() stream
+std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off);
+// host float queries [nq][dim] -> prepared device rows (Index::allocateObject)
+int upload_queries(ngt_amd_index* ix, const void* queries, uint32_t nq, DevBuf<float>& raw,
+                   DevBuf<uint8_t>& prep, hipStream_t s);
+
+}  // namespace ngt_amd

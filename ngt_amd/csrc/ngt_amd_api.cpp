@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/ngt_amd.h"
+#include "index_internal.h"
 #include "ngt_kernels.h"
 #include "prep_kernels.h"
 
@@ -25,7 +26,7 @@ using namespace ngt_amd;
 
 static thread_local std::string g_err;
 
-static int fail(const char* fmt, ...) {
+int ngt_amd::fail(const char* fmt, ...) {
   char buf[1024];
   va_list ap;
   va_start(ap, fmt);
@@ -34,84 +35,6 @@ static int fail(const char* fmt, ...) {
   g_err = buf;
   return -1;
 }
-
-#define HIP_OK(expr)                                                                     \
-  do {                                                                                   \
-    hipError_t e_ = (expr);                                                              \
-    if (e_ != hipSuccess)                                                                \
-      return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
-  } while (0)
-
-template <typename T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  bool owned = true;
-  ~DevBuf() { release(); }
-  void release() {
-    if (p && owned) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-    owned = true;
-  }
-  hipError_t alloc(size_t count) {
-    if (p && owned && n >= count) return hipSuccess;
-    release();
-    n = count;
-    return hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
-  }
-  hipError_t upload(const T* h, size_t count) {
-    hipError_t e = alloc(count);
-    if (e != hipSuccess) return e;
-    if (count) e = hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice);
-    return e;
-  }
-};
-
-struct ngt_amd_index {
-  int device = 0;
-  int metric = 1;
-  int otype = 2;
-  uint32_t dim = 0;
-  uint32_t dp = 0;
-  uint32_t esize = 4;
-  uint64_t row_bytes = 0;
-  uint64_t nrows = 0;
-  DevBuf<uint8_t> rows, valid;
-  std::vector<uint8_t> h_valid;
-  std::vector<uint64_t> h_degree_nonzero;  // for isEmpty in getRandomSeeds
-  DevBuf<uint64_t> edge_off;
-  DevBuf<uint32_t> edges;
-  uint64_t nedges = 0;
-  DevBuf<uint32_t> adj;          // padded fixed-stride copy of the adjacency
-  uint64_t adj_stride = 0;
-  bool has_graph = false;
-  std::vector<uint8_t> h_graph_empty;
-  // tree
-  bool has_tree = false;
-  DevBuf<uint8_t> in_pivot;
-  DevBuf<uint32_t> in_child, leaf_ids;
-  DevBuf<float> in_border;
-  DevBuf<uint64_t> leaf_off;
-  uint32_t children = 5, root = 0;
-  // property
-  int32_t edge_size_for_search = 0;
-  int32_t dyn_base = 30, dyn_rate = 20;
-  int32_t seed_size = 10, seed_type = 0;
-  // scratch
-  DevBuf<uint32_t> work, seeds, seed_count, slot_epoch;
-  DevBuf<uint8_t> vis;
-  DevBuf<uint64_t> spill, seed_off;
-  DevBuf<int> error;
-  uint32_t slots = 0;
-  uint64_t vis_stride = 0;
-  uint32_t spill_cap = 1u << 16;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  float last_ms = 0.f;
-  int cu_count = 256;
-  size_t lds_per_cu = 160 * 1024;
-};
 
 extern "C" const char* ngt_amd_last_error(void) { return g_err.c_str(); }
 
@@ -216,6 +139,7 @@ static void note_graph_empty(ngt_amd_index* ix, const uint64_t* offsets, uint64_
 static int build_padded_adjacency(ngt_amd_index* ix, const uint64_t* h_offsets) {
   uint64_t maxdeg = 0;
   for (uint64_t i = 0; i < ix->nrows; i++) maxdeg = std::max<uint64_t>(maxdeg, h_offsets[i + 1] - h_offsets[i]);
+  ix->max_degree = maxdeg;
   ix->adj.release();
   ix->adj_stride = 0;
   if (maxdeg == 0 || maxdeg > 256) return 0;
@@ -292,7 +216,7 @@ extern "C" int ngt_amd_index_set_search_property(ngt_amd_index* ix, int32_t edge
   return 0;
 }
 
-static float coef_of(float epsilon) {
+float ngt_amd::coef_of(float epsilon) {
   // SearchContainer::setEpsilon (Common.h:2041); 0 => NGT_EXPLORATION_COEFFICIENT (Graph.cpp:403-405)
   float c = (float)((double)epsilon + 1.0);
   if (c == 0.0f) c = (float)1.1;
@@ -312,9 +236,10 @@ extern "C" uint64_t ngt_amd_resolve_edge_size(const ngt_amd_index* ix, int64_t e
   return 0;  // invalid -> caller reports
 }
 
-static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a, hipStream_t s) {
-  size_t lds = search_lds_bytes(a, ix->otype);
-  if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
+// Per-slot scratch of the persistent search kernels (slot = resident wave):
+// visited-epoch bytes, their epochs and the unchecked-set spill.  Sized by the
+// LDS footprint of one slot, which bounds how many are resident per CU.
+int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, size_t lds, hipStream_t s) {
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
   if (per_cu > 16) per_cu = 16;
   if (per_cu < 1) per_cu = 1;
@@ -332,6 +257,37 @@ static int ensure_scratch(ngt_amd_index* ix, const SearchArgs& a, hipStream_t s)
     ix->slots = slots;
     ix->vis_stride = stride;
   }
+  return 0;
+}
+
+// GraphAndTreeIndex::getSeedsFromTree (Index.h:1524-1567) for a batch: seed
+// lists land in ix->seeds ([nq][kTreeSeedStride]) and ix->seed_count.
+int ngt_amd::run_tree_seeds(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq,
+                            uint32_t k, int all_leaf_nodes, hipStream_t s) {
+  if (!ix->has_tree) return fail("search: tree seeds requested but the index has no tree");
+  const uint32_t stride = kTreeSeedStride;
+  HIP_OK(ix->seeds.alloc((size_t)nq * stride));
+  HIP_OK(ix->seed_count.alloc(nq));
+  TreeSeedArgs t{};
+  t.queries = static_cast<const uint8_t*>(d_queries);
+  t.query_bytes = query_bytes;
+  t.nq = nq;
+  t.dp = (int)ix->dp;
+  t.row_bytes = ix->row_bytes;
+  t.in_pivot = ix->in_pivot.p;
+  t.in_child = ix->in_child.p;
+  t.in_border = ix->in_border.p;
+  t.children = ix->children;
+  t.root = ix->root;
+  t.leaf_off = ix->leaf_off.p;
+  t.leaf_ids = ix->leaf_ids.p;
+  t.seed_size = (uint32_t)std::max(ix->seed_size, 0);
+  t.k = k;
+  t.all_leaf_nodes = all_leaf_nodes || ix->seed_type == 4;
+  t.seeds = ix->seeds.p;
+  t.seed_stride = stride;
+  t.seed_count = ix->seed_count.p;
+  HIP_OK(launch_tree_seeds(t, ix->metric, ix->otype, s));
   return 0;
 }
 
@@ -378,39 +334,18 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
   a.error = ix->error.p;
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
-    if (!ix->has_tree) return fail("search: tree seeds requested but the index has no tree");
-    const uint32_t stride = 128;
-    HIP_OK(ix->seeds.alloc((size_t)nq * stride));
-    HIP_OK(ix->seed_count.alloc(nq));
-    TreeSeedArgs t{};
-    t.queries = a.queries;
-    t.query_bytes = query_bytes;
-    t.nq = nq;
-    t.dp = a.dp;
-    t.row_bytes = ix->row_bytes;
-    t.in_pivot = ix->in_pivot.p;
-    t.in_child = ix->in_child.p;
-    t.in_border = ix->in_border.p;
-    t.children = ix->children;
-    t.root = ix->root;
-    t.leaf_off = ix->leaf_off.p;
-    t.leaf_ids = ix->leaf_ids.p;
-    t.seed_size = (uint32_t)std::max(ix->seed_size, 0);
-    t.k = prm->k;
-    t.all_leaf_nodes = prm->all_leaf_nodes || ix->seed_type == 4;
-    t.seeds = ix->seeds.p;
-    t.seed_stride = stride;
-    t.seed_count = ix->seed_count.p;
-    HIP_OK(launch_tree_seeds(t, ix->metric, ix->otype, s));
+    if (run_tree_seeds(ix, d_queries, query_bytes, nq, prm->k, prm->all_leaf_nodes, s)) return -1;
     a.seeds = ix->seeds.p;
-    a.seed_stride = stride;
+    a.seed_stride = kTreeSeedStride;
     a.seed_count = ix->seed_count.p;
   } else {
     if (!d_seeds || !d_seed_off) return fail("search: seed lists required for this seed mode");
     a.seeds = d_seeds;
     a.seed_off = d_seed_off;
   }
-  if (ensure_scratch(ix, a, s)) return -1;
+  const size_t lds = search_lds_bytes(a, ix->otype);
+  if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
+  if (ensure_vis_scratch(ix, lds, s)) return -1;
   a.vis = ix->vis.p;
   a.vis_stride = ix->vis_stride;
   a.slot_epoch = ix->slot_epoch.p;
@@ -425,7 +360,7 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
   return 0;
 }
 
-static std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off) {
+std::vector<uint32_t> ngt_amd::random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off) {
   // GraphIndex::getRandomSeeds (Index.h:775-801) over the process-wide rand()
   // stream, one query after another as the reference's callers do.
   std::vector<uint32_t> seeds;
@@ -479,7 +414,7 @@ extern "C" float ngt_amd_last_search_kernel_ms(const ngt_amd_index* ix) {
 }
 
 // Upload host float queries and prepare them on the device.
-static int upload_queries(ngt_amd_index* ix, const void* queries, uint32_t nq, DevBuf<float>& raw,
+int ngt_amd::upload_queries(ngt_amd_index* ix, const void* queries, uint32_t nq, DevBuf<float>& raw,
                           DevBuf<uint8_t>& prep, hipStream_t s) {
   // host queries are float [nq][dim] for every object type (Index::allocateObject
   // converts them to the object type, ObjectRepository.h:222-253)

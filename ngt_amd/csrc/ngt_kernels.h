@@ -101,4 +101,96 @@ hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint3
 hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint32_t nslices,
                                 hipStream_t s);
 
+// ---- NGTQG (qg_kernels.hip) ------------------------------------------------
+struct QgLutArgs {
+  const uint8_t* queries;        // prepared float query rows (padded dp)
+  uint64_t query_bytes;
+  uint32_t nq;
+  const float* global;           // [D] global centroid
+  const float* local;            // [M][16][dsub] local centroids (ids 1..16)
+  uint32_t M, dsub, Me;          // Me = M rounded up to even
+  uint8_t* lut;                  // [nq][lut_stride], lut_stride >= Me*16
+  uint64_t lut_stride;
+  float* scale;                  // [nq]
+  float* toff;                   // [nq] totalOffset
+};
+
+struct QgBuildArgs {
+  const uint64_t* edge_off;      // graph CSR [nrows+1]
+  const uint32_t* edges;
+  uint32_t nrows;
+  uint32_t max_edges;
+  const uint8_t* local_codes;    // [nrows][M] localID - 1 (0..15)
+  uint32_t M, Me;
+  uint32_t* qids;                // [nrows][id_stride], 0-terminated
+  uint32_t id_stride;
+  uint8_t* qcodes;               // [nrows][code_stride]
+  uint64_t code_stride;          // (id_stride / 16) * 8 * Me
+};
+
+struct QgAdcArgs {
+  const uint32_t* qids;
+  uint32_t id_stride;
+  const uint8_t* qcodes;
+  uint64_t code_stride;
+  uint32_t Me;
+  const uint8_t* lut;
+  uint64_t lut_stride;
+  const float* scale;
+  const float* toff;
+  const uint32_t* qidx;          // per pair: query
+  const uint32_t* node;          // per pair: node whose neighbour list is scored
+  uint64_t npairs;
+  float* out;                    // [npairs][out_stride]
+  uint32_t out_stride;
+  uint32_t* out_n;               // [npairs] neighbour count
+};
+
+struct QgSearchArgs {
+  const uint8_t* rows;           // exact rows (seeds, rerank)
+  uint64_t row_bytes;
+  uint32_t nrows;
+  int dp;
+  const uint32_t* qids;
+  uint32_t id_stride;
+  const uint8_t* qcodes;
+  uint64_t code_stride;
+  uint32_t Me;
+  const uint8_t* lut;
+  uint64_t lut_stride;
+  const float* scale;
+  const float* toff;
+  const uint8_t* queries;
+  uint64_t query_bytes;
+  uint32_t nq;
+  const uint32_t* seeds;
+  const uint64_t* seed_off;
+  uint32_t seed_stride;
+  const uint32_t* seed_count;
+  uint32_t k;                    // sizeBackup
+  uint32_t size;                 // sc.size after *= resultExpansion
+  int rerank;                    // resultExpansion >= 1
+  float coef;
+  float radius;
+  uint32_t ht_log2;
+  uint32_t cq_cap;
+  uint32_t* out_ids;             // [nq][k]
+  float* out_dists;
+  uint32_t* out_n;
+  uint64_t* counters;            // [nq][8]: ADC, accepted, expansions, exact, code blocks, max queue, spilled
+  uint32_t* work;
+  uint8_t* vis;
+  uint64_t vis_stride;
+  uint32_t* slot_epoch;
+  uint64_t* spill;
+  uint32_t spill_cap;
+  int* error;
+};
+
+hipError_t launch_qg_lut(const QgLutArgs& a, hipStream_t s);
+hipError_t launch_qg_build(const QgBuildArgs& a, hipStream_t s);
+hipError_t launch_qg_adc(const QgAdcArgs& a, hipStream_t s);
+size_t qg_search_lds_bytes(const QgSearchArgs& a);
+hipError_t launch_qg_search(const QgSearchArgs& a, uint32_t slots, hipStream_t s);
+
 }  // namespace ngt_amd

@@ -1,0 +1,352 @@
+// qg_api.cpp -- host side of the NGTQG entry points of include/ngt_amd.h.
+//
+// The quantized graph of an index lives in HBM as two fixed-stride slabs:
+//   qids   [nrows][id_stride]   neighbour ids, 0-terminated (id_stride =
+//                               max degree rounded up to 16)
+//   qcodes [nrows][code_stride] packed 4-bit codes, (id_stride/16) blocks of
+//                               8*Me bytes in the reference stream layout
+//                               (Quantizer.h:1295-1327)
+// so an expansion addresses both from the node id alone.  Every ADC and
+// every search runs on the device (qg_kernels.hip); there is no CPU path.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <vector>
+
+#include "../../include/ngt_amd.h"
+#include "index_internal.h"
+#include "ngt_kernels.h"
+
+using namespace ngt_amd;
+
+static const uint32_t kMaxMe = 512;  // packed u16 sums exact up to Me = 514
+
+extern "C" int ngt_amd_qg_set_quantizer(ngt_amd_index* ix, const float* global, const float* local, uint32_t M,
+                                        uint32_t dsub) {
+  if (!ix || !global || !local || M == 0 || dsub == 0) return fail("ngt_amd_qg_set_quantizer: bad arguments");
+  if (ix->metric != NGT_AMD_DISTANCE_L2 || ix->otype != NGT_AMD_OBJECT_FLOAT)
+    return fail("ngt_amd_qg_set_quantizer: NGTQG needs an L2 float index");
+  if ((uint64_t)M * dsub != ix->dim)
+    return fail("ngt_amd_qg_set_quantizer: M (%u) x dsub (%u) != dimension (%u)", M, dsub, ix->dim);
+  const uint32_t Me = (M + 1) / 2 * 2;
+  if (Me > kMaxMe) return fail("ngt_amd_qg_set_quantizer: %u subspaces exceed the supported %u", M, kMaxMe);
+  HIP_OK(hipSetDevice(ix->device));
+  QgState& q = ix->qg;
+  HIP_OK(q.global.upload(global, ix->dim));
+  HIP_OK(q.local.upload(local, (size_t)M * 16 * dsub));
+  if (q.M != M) {
+    q.qids.release();
+    q.qcodes.release();
+    q.has_graph = false;
+  }
+  q.M = M;
+  q.dsub = dsub;
+  q.Me = Me;
+  q.ready = true;
+  return 0;
+}
+
+static int alloc_qg_graph(ngt_amd_index* ix, uint64_t maxdeg) {
+  QgState& q = ix->qg;
+  const uint32_t stride = (uint32_t)std::max<uint64_t>(16, (maxdeg + 15) & ~15ull);
+  if (stride > 256) return fail("qg graph: %llu neighbours per node exceed the supported 256",
+                                (unsigned long long)maxdeg);
+  q.id_stride = stride;
+  q.code_stride = (uint64_t)(stride / 16) * 8 * q.Me;
+  HIP_OK(q.qids.alloc((size_t)ix->nrows * q.id_stride));
+  HIP_OK(q.qcodes.alloc((size_t)ix->nrows * q.code_stride));
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_build_graph(ngt_amd_index* ix, const uint8_t* local_codes, uint32_t max_edges) {
+  if (!ix || !local_codes || max_edges == 0) return fail("ngt_amd_qg_build_graph: bad arguments");
+  if (!ix->qg.ready) return fail("ngt_amd_qg_build_graph: set the quantizer first");
+  if (!ix->has_graph) return fail("ngt_amd_qg_build_graph: the index has no graph");
+  HIP_OK(hipSetDevice(ix->device));
+  QgState& q = ix->qg;
+  if (alloc_qg_graph(ix, std::min<uint64_t>(ix->max_degree, max_edges))) return -1;
+  DevBuf<uint8_t> codes;
+  HIP_OK(codes.upload(local_codes, (size_t)ix->nrows * q.M));
+  QgBuildArgs a{};
+  a.edge_off = ix->edge_off.p;
+  a.edges = ix->edges.p;
+  a.nrows = (uint32_t)ix->nrows;
+  a.max_edges = max_edges;
+  a.local_codes = codes.p;
+  a.M = q.M;
+  a.Me = q.Me;
+  a.qids = q.qids.p;
+  a.id_stride = q.id_stride;
+  a.qcodes = q.qcodes.p;
+  a.code_stride = q.code_stride;
+  HIP_OK(launch_qg_build(a, ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  q.has_graph = true;
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_set_graph(ngt_amd_index* ix, const uint64_t* qoff, const uint32_t* qids,
+                                    const uint64_t* code_off, const uint8_t* codes) {
+  if (!ix || !qoff || !code_off) return fail("ngt_amd_qg_set_graph: bad arguments");
+  if (!ix->qg.ready) return fail("ngt_amd_qg_set_graph: set the quantizer first");
+  if (ix->nrows == 0) return fail("ngt_amd_qg_set_graph: set the objects first");
+  HIP_OK(hipSetDevice(ix->device));
+  QgState& q = ix->qg;
+  const uint64_t n = ix->nrows;
+  uint64_t maxdeg = 0;
+  for (uint64_t v = 0; v < n; v++) {
+    const uint64_t deg = qoff[v + 1] - qoff[v];
+    const uint64_t nb = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+    if (code_off[v + 1] - code_off[v] != nb * 8 * q.Me)
+      return fail("ngt_amd_qg_set_graph: node %llu has %llu code bytes, expected %llu", (unsigned long long)v,
+                  (unsigned long long)(code_off[v + 1] - code_off[v]), (unsigned long long)(nb * 8 * q.Me));
+    for (uint64_t i = qoff[v]; i < qoff[v + 1]; i++)
+      if (qids[i] == 0 || qids[i] >= n) return fail("ngt_amd_qg_set_graph: neighbour id %u out of range", qids[i]);
+    maxdeg = std::max(maxdeg, deg);
+  }
+  if (alloc_qg_graph(ix, maxdeg)) return -1;
+  std::vector<uint32_t> hid((size_t)n * q.id_stride, 0u);
+  std::vector<uint8_t> hcode((size_t)n * q.code_stride, 0u);
+  for (uint64_t v = 0; v < n; v++) {
+    std::copy(qids + qoff[v], qids + qoff[v + 1], hid.begin() + v * q.id_stride);
+    std::copy(codes + code_off[v], codes + code_off[v + 1], hcode.begin() + v * q.code_stride);
+  }
+  HIP_OK(hipMemcpy(q.qids.p, hid.data(), hid.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(q.qcodes.p, hcode.data(), hcode.size(), hipMemcpyHostToDevice));
+  q.has_graph = true;
+  return 0;
+}
+
+extern "C" uint32_t ngt_amd_qg_max_degree(const ngt_amd_index* ix) {
+  return ix && ix->qg.has_graph ? ix->qg.id_stride : 0;
+}
+
+// LUTs of nq prepared device queries into ix->qg.lut/scale/toff.
+static int run_lut(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq, hipStream_t s) {
+  QgState& q = ix->qg;
+  HIP_OK(q.lut.alloc((size_t)nq * q.Me * 16));
+  HIP_OK(q.scale.alloc(nq));
+  HIP_OK(q.toff.alloc(nq));
+  QgLutArgs a{};
+  a.queries = static_cast<const uint8_t*>(d_queries);
+  a.query_bytes = query_bytes;
+  a.nq = nq;
+  a.global = q.global.p;
+  a.local = q.local.p;
+  a.M = q.M;
+  a.dsub = q.dsub;
+  a.Me = q.Me;
+  a.lut = q.lut.p;
+  a.lut_stride = (uint64_t)q.Me * 16;
+  a.scale = q.scale.p;
+  a.toff = q.toff.p;
+  HIP_OK(launch_qg_lut(a, s));
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_lut(ngt_amd_index* ix, const float* queries, uint32_t nq, uint8_t* lut, float* scale,
+                              float* total_offset) {
+  if (!ix || (!queries && nq) || !lut || !scale || !total_offset) return fail("ngt_amd_qg_lut: bad arguments");
+  if (!ix->qg.ready) return fail("ngt_amd_qg_lut: the index has no quantizer");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = ix->stream;
+  DevBuf<float> raw;
+  DevBuf<uint8_t> prep;
+  if (upload_queries(ix, queries, nq, raw, prep, s)) return -1;
+  if (run_lut(ix, prep.p, ix->row_bytes, nq, s)) return -1;
+  const QgState& q = ix->qg;
+  HIP_OK(hipMemcpyAsync(lut, q.lut.p, (size_t)nq * q.Me * 16, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(scale, q.scale.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(total_offset, q.toff.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_adc(ngt_amd_index* ix, const uint8_t* lut, const float* scale, const float* total_offset,
+                              uint32_t nq, const uint32_t* qidx, const uint32_t* node, uint64_t npairs, float* out,
+                              uint32_t* out_n) {
+  if (!ix || !lut || !scale || !total_offset || !qidx || !node || !out || !out_n)
+    return fail("ngt_amd_qg_adc: bad arguments");
+  if (!ix->qg.has_graph) return fail("ngt_amd_qg_adc: the index has no quantized graph");
+  if (npairs == 0) return 0;
+  for (uint64_t i = 0; i < npairs; i++) {
+    if (qidx[i] >= nq) return fail("ngt_amd_qg_adc: query index %u out of range", qidx[i]);
+    if (node[i] >= ix->nrows) return fail("ngt_amd_qg_adc: node %u out of range", node[i]);
+  }
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = ix->stream;
+  const QgState& q = ix->qg;
+  DevBuf<uint8_t> dl;
+  DevBuf<float> dsc, dto, dout;
+  DevBuf<uint32_t> dq, dn, dcnt;
+  HIP_OK(dl.upload(lut, (size_t)nq * q.Me * 16));
+  HIP_OK(dsc.upload(scale, nq));
+  HIP_OK(dto.upload(total_offset, nq));
+  HIP_OK(dq.upload(qidx, npairs));
+  HIP_OK(dn.upload(node, npairs));
+  HIP_OK(dout.alloc((size_t)npairs * q.id_stride));
+  HIP_OK(dcnt.alloc(npairs));
+  QgAdcArgs a{};
+  a.qids = q.qids.p;
+  a.id_stride = q.id_stride;
+  a.qcodes = q.qcodes.p;
+  a.code_stride = q.code_stride;
+  a.Me = q.Me;
+  a.lut = dl.p;
+  a.lut_stride = (uint64_t)q.Me * 16;
+  a.scale = dsc.p;
+  a.toff = dto.p;
+  a.qidx = dq.p;
+  a.node = dn.p;
+  a.npairs = npairs;
+  a.out = dout.p;
+  a.out_stride = q.id_stride;
+  a.out_n = dcnt.p;
+  HIP_OK(hipMemsetAsync(dout.p, 0, (size_t)npairs * q.id_stride * sizeof(float), s));
+  HIP_OK(launch_qg_adc(a, s));
+  HIP_OK(hipMemcpyAsync(out, dout.p, (size_t)npairs * q.id_stride * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(out_n, dcnt.p, npairs * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_search_params* prm,
+                                        const void* d_queries, uint64_t query_bytes, uint32_t nq,
+                                        const uint32_t* d_seeds, const uint64_t* d_seed_off, uint32_t* d_ids,
+                                        float* d_dists, uint32_t* d_n, uint64_t* d_counters, void* stream) {
+  if (!ix || !prm || (!d_queries && nq)) return fail("ngt_amd_qg_search_device: bad arguments");
+  if (!ix->qg.has_graph) return fail("ngt_amd_qg_search: the index has no quantized graph");
+  if (prm->k == 0) return fail("ngt_amd_qg_search: k must be > 0");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = (hipStream_t)stream;
+  QgState& q = ix->qg;
+
+  QgSearchArgs a{};
+  a.rows = ix->rows.p;
+  a.row_bytes = ix->row_bytes;
+  a.nrows = (uint32_t)ix->nrows;
+  a.dp = (int)ix->dp;
+  a.qids = q.qids.p;
+  a.id_stride = q.id_stride;
+  a.qcodes = q.qcodes.p;
+  a.code_stride = q.code_stride;
+  a.Me = q.Me;
+  a.queries = static_cast<const uint8_t*>(d_queries);
+  a.query_bytes = query_bytes;
+  a.nq = nq;
+  a.k = prm->k;
+  // sc.size *= resultExpansion: size_t * float -> float -> size_t (QuantizedGraph.h:194-196)
+  uint64_t size = prm->k;
+  if (prm->result_expansion > 1.0f) size = (uint64_t)((float)size * prm->result_expansion);
+  if (size == 0) return fail("ngt_amd_qg_search: empty result size");
+  a.size = (uint32_t)size;
+  a.rerank = prm->result_expansion >= 1.0f;
+  a.coef = coef_of(prm->epsilon);
+  a.radius = prm->radius < 0.0f ? FLT_MAX : prm->radius;
+  a.ht_log2 = 12;
+  a.cq_cap = 1024;
+  if (prm->visited_hash_log2 < 0) a.ht_log2 = 0;
+  else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
+  if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
+  if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+  a.out_ids = d_ids;
+  a.out_dists = d_dists;
+  a.out_n = d_n;
+  a.counters = d_counters;
+  a.error = ix->error.p;
+
+  if (prm->seed_mode == NGT_AMD_SEED_TREE) {
+    // getSeedsFromTree with the caller's k (before the expansion, :362)
+    if (run_tree_seeds(ix, d_queries, query_bytes, nq, prm->k, 0, s)) return -1;
+    a.seeds = ix->seeds.p;
+    a.seed_stride = kTreeSeedStride;
+    a.seed_count = ix->seed_count.p;
+  } else if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
+    HIP_OK(ix->seed_off.upload(off.data(), off.size()));
+    HIP_OK(ix->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
+    a.seeds = ix->seeds.p;
+    a.seed_off = ix->seed_off.p;
+  } else {
+    if (!d_seeds || !d_seed_off) return fail("ngt_amd_qg_search: seed lists required for this seed mode");
+    a.seeds = d_seeds;
+    a.seed_off = d_seed_off;
+  }
+  if (run_lut(ix, d_queries, query_bytes, nq, s)) return -1;
+  a.lut = q.lut.p;
+  a.lut_stride = (uint64_t)q.Me * 16;
+  a.scale = q.scale.p;
+  a.toff = q.toff.p;
+
+  const size_t lds = qg_search_lds_bytes(a);
+  if (lds > 64 * 1024)
+    return fail("ngt_amd_qg_search: k=%u x expansion needs %zu bytes of LDS per query (max 65536)", a.k, lds);
+  if (ensure_vis_scratch(ix, lds, s)) return -1;
+  a.vis = ix->vis.p;
+  a.vis_stride = ix->vis_stride;
+  a.slot_epoch = ix->slot_epoch.p;
+  a.spill = ix->spill.p;
+  a.spill_cap = ix->spill_cap;
+  a.work = ix->work.p;
+  HIP_OK(hipMemsetAsync(ix->work.p, 0, sizeof(uint32_t), s));
+  const uint32_t slots = std::min<uint32_t>(ix->slots, nq);
+  HIP_OK(hipEventRecord(ix->ev0, s));
+  HIP_OK(launch_qg_search(a, slots, s));
+  HIP_OK(hipEventRecord(ix->ev1, s));
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_search(ngt_amd_index* ix, const ngt_amd_qg_search_params* prm, const float* queries,
+                                 uint32_t nq, const uint32_t* seeds, const uint64_t* seed_off, uint32_t* ids,
+                                 float* dists, uint32_t* n, uint64_t* counters) {
+  if (!ix || !prm || (!queries && nq) || !ids || !dists || !n) return fail("ngt_amd_qg_search: bad arguments");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = ix->stream;
+  DevBuf<float> raw;
+  DevBuf<uint8_t> qb;
+  if (upload_queries(ix, queries, nq, raw, qb, s)) return -1;
+  DevBuf<uint32_t> d_ids, d_n, d_seeds;
+  DevBuf<float> d_dists;
+  DevBuf<uint64_t> d_cnt, d_seed_off;
+  HIP_OK(d_ids.alloc((size_t)nq * prm->k));
+  HIP_OK(d_dists.alloc((size_t)nq * prm->k));
+  HIP_OK(d_n.alloc(nq));
+  if (counters) HIP_OK(d_cnt.alloc((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY));
+  const uint32_t* sp = nullptr;
+  const uint64_t* so = nullptr;
+  if (prm->seed_mode == NGT_AMD_SEED_GIVEN) {
+    if (!seeds || !seed_off) return fail("ngt_amd_qg_search: NGT_AMD_SEED_GIVEN needs seeds and seed_off");
+    for (uint64_t i = 0; i < seed_off[nq]; i++)
+      if (seeds[i] == 0 || seeds[i] >= ix->nrows) return fail("ngt_amd_qg_search: seed id %u out of range", seeds[i]);
+    HIP_OK(d_seeds.upload(seeds, std::max<uint64_t>(seed_off[nq], 1)));
+    HIP_OK(d_seed_off.upload(seed_off, (size_t)nq + 1));
+    sp = d_seeds.p;
+    so = d_seed_off.p;
+  }
+  if (ngt_amd_qg_search_device(ix, prm, qb.p, ix->row_bytes, nq, sp, so, d_ids.p, d_dists.p, d_n.p,
+                               counters ? d_cnt.p : nullptr, s))
+    return -1;
+  HIP_OK(hipMemcpyAsync(ids, d_ids.p, (size_t)nq * prm->k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(dists, d_dists.p, (size_t)nq * prm->k * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(n, d_n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (counters)
+    HIP_OK(hipMemcpyAsync(counters, d_cnt.p, (size_t)nq * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
+                          hipMemcpyDeviceToHost, s));
+  int herr = 0;
+  HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  if (herr) {
+    (void)hipMemset(ix->error.p, 0, sizeof(int));
+    return fail("ngt_amd_qg_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
+  }
+  return 0;
+}

@@ -1,0 +1,653 @@
+// qg_kernels.hip -- gfx950 kernels for the NGTQG quantized-graph path.
+//
+//  * ngt_qg_lut_kernel   : QuantizedObjectDistance::createDistanceLookup
+//                          (lib/NGT/NGTQ/Quantizer.h:709-760) over
+//                          createFloatL2DistanceLookup (:683-706) -- the
+//                          per-query uint8 table, scale and totalOffset.
+//  * ngt_qg_build_kernel : QuantizedGraphRepository::construct
+//                          (lib/NGT/NGTQ/QuantizedGraph.h:64-115) with the
+//                          stream layout of QuantizedObjectProcessingStream
+//                          (Quantizer.h:1268-1327), into fixed-stride rows.
+//  * ngt_qg_adc_kernel   : QuantizedObjectDistanceFloat::operator()
+//                          (Quantizer.h:957-1062) over whole neighbour lists.
+//  * ngt_qg_search_kernel: NGTQG::Index::searchQuantizedGraph
+//                          (QuantizedGraph.h:192-320), one wave per query.
+//
+// 4-bit ADC on CDNA4: the reference shuffles 16-entry byte tables with
+// pshufb.  Here lane l owns subspace pair p = l (+64 s): its two 16-byte
+// table rows sit in 8 VGPRs and a lookup of four nibbles is two v_perm_b32
+// (8-byte tables) plus a byte select on bit 3.  A 16-object block is 8*Me
+// bytes: the 16 bytes of pair p are contiguous at 16p, so one wave-wide
+// 16-byte load streams a whole 1 KiB block (M = 128).  Per-object sums are
+// packed (even subspaces | odd subspaces << 16), exactly the reference's two
+// u16 accumulators, and reduce-scattered across the wave in 17 shuffles
+// (16 values -> 1 per lane) instead of 16 full wave reductions.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ngt_device.h"
+#include "ngt_kernels.h"
+#include "search_common.h"
+
+namespace ngt_amd {
+
+// ---------------------------------------------------------------------------
+// LUT: one wave per query.  d[m][c] = sum_j fma((q - g - C[m][c])^2) in float
+// (the -Ofast reference contracts the sum into an FMA chain), one global
+// min/max, quantised with roundf((d - min) / scale).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) ngt_qg_lut_kernel(QgLutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float* d = reinterpret_cast<float*>(smem);
+  const int lane = lane_id();
+  const uint32_t n = a.M * 16;
+  for (uint32_t qi = blockIdx.x; qi < a.nq; qi += gridDim.x) {
+    const float* q = reinterpret_cast<const float*>(a.queries + (uint64_t)qi * a.query_bytes);
+    float mn = __int_as_float(0x7f7fffff), mx = -__int_as_float(0x7f7fffff);  // FLT_MAX, -FLT_MAX
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t m = i >> 4, c = i & 15;
+      const float* qq = q + (uint64_t)m * a.dsub;
+      const float* gg = a.global + (uint64_t)m * a.dsub;
+      const float* lc = a.local + ((uint64_t)m * 16 + c) * a.dsub;
+      float acc = 0.0f;
+      for (uint32_t j = 0; j < a.dsub; j++) {
+        const float sub = (qq[j] - gg[j]) - lc[j];
+        acc = __builtin_fmaf(sub, sub, acc);
+      }
+      d[i] = acc;
+      mx = acc > mx ? acc : mx;
+      mn = acc < mn ? acc : mn;
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+      const float omx = __shfl_xor(mx, s, 64), omn = __shfl_xor(mn, s, 64);
+      mx = omx > mx ? omx : mx;
+      mn = omn < mn ? omn : mn;
+    }
+    __syncthreads();
+    const float offset = mn;
+    const float scale = (float)((double)(mx - mn) / 255.0);  // (Quantizer.h:738)
+    uint8_t* out = a.lut + (uint64_t)qi * a.lut_stride;
+    for (uint32_t i = lane; i < a.Me * 16; i += 64) {
+      uint8_t v = 0;  // the odd-M pad subspace is zero (:751-757)
+      if (i < n) {
+        const float t = (d[i] - offset) / scale;
+        // (int32_t)round(x) then uint8 truncation; a NaN quotient (scale 0)
+        // converts to INT_MIN on x86, whose low byte is 0
+        v = (t == t) ? (uint8_t)(int32_t)roundf(t) : (uint8_t)0;
+      }
+      out[i] = v;
+    }
+    if (lane == 0) {
+      float tot = 0.0f;
+      for (uint32_t m = 0; m < a.M; m++) tot += offset;  // totalOffset (:749)
+      a.scale[qi] = scale;
+      a.toff[qi] = tot;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Quantized graph construction: node v keeps its first min(deg, max_edges)
+// graph edges in stored order; codes = localID - 1 per subspace, arranged per
+// 16-object block as byte (8m + j) = obj(2j) | obj(2j+1) << 4.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) ngt_qg_build_kernel(QgBuildArgs a) {
+  const uint32_t warps = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const uint64_t blk = (uint64_t)8 * a.Me;
+  for (uint32_t v = w0; v < a.nrows; v += warps) {
+    const uint64_t eb = a.edge_off[v];
+    uint64_t deg = a.edge_off[v + 1] - eb;
+    if (deg > a.max_edges) deg = a.max_edges;
+    uint32_t* ids = a.qids + (uint64_t)v * a.id_stride;
+    for (uint32_t i = lane; i < a.id_stride; i += 64) ids[i] = i < deg ? a.edges[eb + i] : 0u;
+    uint8_t* codes = a.qcodes + (uint64_t)v * a.code_stride;
+    const uint64_t nb = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+    for (uint64_t t = lane; t < a.code_stride; t += 64) {
+      uint8_t byte = 0;
+      const uint64_t b = t / blk;
+      if (b < nb) {
+        const uint64_t r = t - b * blk;
+        const uint32_t m = (uint32_t)(r >> 3), j = (uint32_t)(r & 7);
+        const uint64_t o0 = b * 16 + 2 * j, o1 = o0 + 1;
+        if (m < a.M) {
+          if (o0 < deg) byte |= (uint8_t)(a.local_codes[(uint64_t)a.edges[eb + o0] * a.M + m] & 15);
+          if (o1 < deg) byte |= (uint8_t)((a.local_codes[(uint64_t)a.edges[eb + o1] * a.M + m] & 15) << 4);
+        }
+      }
+      codes[t] = byte;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ADC building blocks.
+// ---------------------------------------------------------------------------
+// Four table lookups: bytes of `idx` (each 0..15) index the 16-byte table
+// t0..t3 (little-endian dwords).
+__device__ __forceinline__ uint32_t lut16(uint32_t idx, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3) {
+  const uint32_t sel = idx & 0x07070707u;
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, sel);
+  const uint32_t hi = __builtin_amdgcn_perm(t3, t2, sel);
+  const uint32_t m = ((idx >> 3) & 0x01010101u) * 0xffu;
+  return (hi & m) | (lo & ~m);
+}
+
+// Lane table of PPL subspace pairs: tab[s][0..3] even subspace 2p, [4..7] odd 2p+1.
+template <int PPL>
+struct LaneLut {
+  uint32_t t[PPL][8];
+};
+
+template <int PPL>
+__device__ __forceinline__ void load_lane_lut(LaneLut<PPL>& L, const uint8_t* lut, uint32_t npairs) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int s = 0; s < PPL; s++) {
+    const uint32_t p = (uint32_t)lane + 64u * s;
+    uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+    if (p < npairs) {
+      const uint4* src = reinterpret_cast<const uint4*>(lut + (uint64_t)p * 32);
+      a = src[0];
+      b = src[1];
+    }
+    L.t[s][0] = a.x; L.t[s][1] = a.y; L.t[s][2] = a.z; L.t[s][3] = a.w;
+    L.t[s][4] = b.x; L.t[s][5] = b.y; L.t[s][6] = b.z; L.t[s][7] = b.w;
+  }
+}
+
+// Packed per-object partial sums of one lane for one block: v[o] =
+// E(o) | O(o) << 16 over this lane's pairs.  c[s]: the 16 code bytes of pair s.
+template <int PPL>
+__device__ __forceinline__ void block_partials(const LaneLut<PPL>& L, const uint4 (&c)[PPL], uint32_t (&v)[16]) {
+#pragma unroll
+  for (int o = 0; o < 16; o++) v[o] = 0;
+#pragma unroll
+  for (int s = 0; s < PPL; s++) {
+    const uint32_t* t = L.t[s];
+    // even subspace: c.x = objects 0..7, c.y = 8..15 (low nibble = even object)
+    const uint32_t e0 = lut16(c[s].x & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);          // 0,2,4,6
+    const uint32_t e1 = lut16((c[s].x >> 4) & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);   // 1,3,5,7
+    const uint32_t e2 = lut16(c[s].y & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);          // 8,...,14
+    const uint32_t e3 = lut16((c[s].y >> 4) & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);   // 9,...,15
+    const uint32_t o0 = lut16(c[s].z & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
+    const uint32_t o1 = lut16((c[s].z >> 4) & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
+    const uint32_t o2 = lut16(c[s].w & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
+    const uint32_t o3 = lut16((c[s].w >> 4) & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
+    // byte b of (e_k, o_k) -> (E | O << 16): selector {b, zero, 4 + b, zero}
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t sel = (uint32_t)b | (12u << 8) | ((4u + b) << 16) | (12u << 24);
+      v[2 * b] += __builtin_amdgcn_perm(o0, e0, sel);
+      v[2 * b + 1] += __builtin_amdgcn_perm(o1, e1, sel);
+      v[8 + 2 * b] += __builtin_amdgcn_perm(o2, e2, sel);
+      v[8 + 2 * b + 1] += __builtin_amdgcn_perm(o3, e3, sel);
+    }
+  }
+}
+
+// Reduce-scatter 16 per-lane values over the wave: on return every lane holds
+// the full sum of object qg_obj_of_lane(lane).
+__device__ __forceinline__ uint32_t reduce_scatter16(uint32_t (&v)[16]) {
+  const int lane = lane_id();
+  {
+    const bool hi = lane & 32;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t send = hi ? v[j] : v[j + 8];
+      const uint32_t keep = hi ? v[j + 8] : v[j];
+      v[j] = keep + (uint32_t)__shfl_xor((int)send, 32, 64);
+    }
+  }
+  {
+    const bool hi = lane & 16;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t send = hi ? v[j] : v[j + 4];
+      const uint32_t keep = hi ? v[j + 4] : v[j];
+      v[j] = keep + (uint32_t)__shfl_xor((int)send, 16, 64);
+    }
+  }
+  {
+    const bool hi = lane & 8;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t send = hi ? v[j] : v[j + 2];
+      const uint32_t keep = hi ? v[j + 2] : v[j];
+      v[j] = keep + (uint32_t)__shfl_xor((int)send, 8, 64);
+    }
+  }
+  {
+    const bool hi = lane & 4;
+    const uint32_t send = hi ? v[0] : v[1];
+    const uint32_t keep = hi ? v[1] : v[0];
+    v[0] = keep + (uint32_t)__shfl_xor((int)send, 4, 64);
+  }
+  uint32_t r = v[0];
+  r += (uint32_t)__shfl_xor((int)r, 2, 64);
+  r += (uint32_t)__shfl_xor((int)r, 1, 64);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t qg_obj_of_lane(int lane) {
+  return (((uint32_t)lane >> 5) & 1) << 3 | (((uint32_t)lane >> 4) & 1) << 2 |
+         (((uint32_t)lane >> 3) & 1) << 1 | (((uint32_t)lane >> 2) & 1);
+}
+
+// sqrtf(fmaf(E + O, scale, totalOffset)) (Quantizer.h:1020-1031).  E and O
+// are the saturating u16 sums; packed partials stay exact while
+// Me/2 * 255 <= 65535 (Me <= 514), which the host enforces.
+__device__ __forceinline__ float adc_epilogue(uint32_t packed, float scale, float toff) {
+  const uint32_t e = packed & 0xffffu, o = packed >> 16;
+  return sqrtf(__builtin_fmaf((float)(e + o), scale, toff));
+}
+
+// ADC of one node's neighbour list: nb blocks at `codes` (8*Me bytes each),
+// distances of objects [0, n) into dists.  The loads of NBF blocks are issued
+// before the first lookup.
+template <int PPL>
+__device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* codes, uint32_t Me, uint32_t n,
+                                         float scale, float toff, float* dists) {
+  const int lane = lane_id();
+  const uint32_t npairs = Me >> 1;
+  const uint32_t nb = n == 0 ? 0 : (n - 1) / 16 + 1;
+  const uint64_t blk = (uint64_t)8 * Me;
+  // blocks whose loads are in flight together (bounded by VGPRs)
+  constexpr int NBF = PPL >= 4 ? 2 : (PPL == 2 ? 4 : 8);
+  for (uint32_t b0 = 0; b0 < nb; b0 += NBF) {
+    uint4 c[NBF][PPL];
+#pragma unroll
+    for (int j = 0; j < NBF; j++) {
+#pragma unroll
+      for (int s = 0; s < PPL; s++) {
+        const uint32_t p = (uint32_t)lane + 64u * s;
+        c[j][s] = make_uint4(0, 0, 0, 0);
+        if (b0 + j < nb && p < npairs)
+          c[j][s] = *reinterpret_cast<const uint4*>(codes + (b0 + j) * blk + (uint64_t)p * 16);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NBF; j++) {
+      if (b0 + j < nb) {
+        uint32_t v[16];
+        block_partials<PPL>(L, c[j], v);
+        const uint32_t r = reduce_scatter16(v);
+        const uint32_t o = (b0 + j) * 16 + qg_obj_of_lane(lane);
+        if ((lane & 3) == 0 && o < n) dists[o] = adc_epilogue(r, scale, toff);
+      }
+    }
+  }
+}
+
+// Standalone ADC: wave per (query, node) pair; out[i*out_stride + j] for the
+// node's neighbours j (full list, the QG loop's call at QuantizedGraph.h:240).
+template <int PPL>
+__global__ void __launch_bounds__(64) ngt_qg_adc_kernel(QgAdcArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float* dd = reinterpret_cast<float*>(smem);
+  const int lane = lane_id();
+  for (uint32_t i = blockIdx.x; i < a.npairs; i += gridDim.x) {
+    const uint32_t qi = a.qidx[i], v = a.node[i];
+    LaneLut<PPL> L;
+    load_lane_lut<PPL>(L, a.lut + (uint64_t)qi * a.lut_stride, a.Me >> 1);
+    const uint32_t* ids = a.qids + (uint64_t)v * a.id_stride;
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < a.id_stride; j += 64)
+      n += (uint32_t)__popcll(ballot64(j + lane < a.id_stride && ids[j + lane] != 0u));
+    adc_node<PPL>(L, a.qcodes + (uint64_t)v * a.code_stride, a.Me, n, a.scale[qi], a.toff[qi], dd);
+    __syncthreads();
+    for (uint32_t j = lane; j < n; j += 64) a.out[(uint64_t)i * a.out_stride + j] = dd[j];
+    if (lane == 0) a.out_n[i] = n;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Quantized-graph search: one wave per query, persistent over a work counter.
+// ---------------------------------------------------------------------------
+// Visited test without insertion (the QG loop tests before it marks).
+__device__ __forceinline__ bool visited_test(uint32_t ht_log2, const uint32_t* ht, uint32_t id, bool vis_mode,
+                                             const uint8_t* vis, uint32_t epoch) {
+  if (vis_mode) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
+    const uint32_t word = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ((word >> (8 * (id & 3))) & 0xffu) == epoch;
+  }
+  const uint32_t mask = (1u << ht_log2) - 1;
+  uint32_t h = ht_hash(id, 32 - ht_log2);
+  for (;;) {
+    const uint32_t old = ht[h];
+    if (old == 0u) return false;
+    if (old == id) return true;
+    h = (h + 1) & mask;
+  }
+}
+
+template <int PPL, int NCH>
+__device__ __forceinline__ void qg_exact(const float* qlds, const QgSearchArgs& a, const uint32_t* ids, float* dists,
+                                         int m) {
+  if constexpr (NCH > 0) {
+    eval_l2f_fast<NCH, 1>(qlds, a.rows, a.row_bytes, ids, dists, m);
+  } else {
+    eval_batch<kL2, float>(qlds, a.rows, a.row_bytes, a.dp, ids, dists, m);
+  }
+}
+
+template <int PPL, int NCH>
+__global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = lane_id();
+  SearchState st;
+  uint8_t* p = smem;
+  const bool use_hash = a.ht_log2 != 0;
+  st.ht = reinterpret_cast<uint32_t*>(p);
+  if (use_hash) p += (size_t)4 << a.ht_log2;
+  st.cq = reinterpret_cast<uint64_t*>(p);
+  p += (size_t)8 * a.cq_cap;
+  st.res = reinterpret_cast<uint64_t*>(p);
+  p += ((size_t)8 * (a.size + 1) + 15) & ~(size_t)15;
+  uint64_t* rr = reinterpret_cast<uint64_t*>(p);  // rerank order
+  p += ((size_t)8 * (a.size + 1) + 15) & ~(size_t)15;
+  const uint32_t nstage = a.id_stride > a.size ? a.id_stride : a.size;
+  const uint32_t nstage64 = (nstage + 63) & ~63u;
+  st.nid = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)4 * nstage64;
+  st.nd = reinterpret_cast<float*>(p);
+  p += (size_t)4 * nstage64;
+  float* qlds = reinterpret_cast<float*>(p);
+
+  const uint32_t slot = blockIdx.x;
+  uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
+  uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
+  const uint32_t hcap = use_hash ? 1u << a.ht_log2 : 0u;
+  const uint32_t hlimit = hcap - (hcap >> 2);
+  const uint32_t npairs = a.Me >> 1;
+
+  for (;;) {
+    uint32_t qi = 0;
+    if (lane == 0) qi = atomicAdd(a.work, 1u);
+    qi = __shfl(qi, 0, 64);
+    if (qi >= a.nq) break;
+
+    for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
+    load_query<float>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
+    LaneLut<PPL> L;
+    load_lane_lut<PPL>(L, a.lut + (uint64_t)qi * a.lut_stride, npairs);
+    const float scale = a.scale[qi], toff = a.toff[qi];
+    uint32_t epoch = a.slot_epoch[slot] + 1;
+    if (epoch > 255) {
+      uint4* v4 = reinterpret_cast<uint4*>(vis);
+      for (uint64_t i = lane; i < a.vis_stride / 16; i += 64) v4[i] = make_uint4(0, 0, 0, 0);
+      epoch = 1;
+    }
+    __syncthreads();
+    if (lane == 0) a.slot_epoch[slot] = epoch;
+
+    bool bitmap_mode = !use_hash;
+    uint32_t nvisited = 0, ncq = 0, nspill = 0, nres = 0, maxq = 0;
+    uint64_t nadc = 0, nacc = 0, nexp = 0, nexact = 0, nblk = 0;
+    const uint32_t size = a.size;
+    float radius = a.radius;
+
+    // ---- setupDistances (exact L2) + setupSeeds (Graph.cpp:293-367) -------
+    const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
+    const uint32_t ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
+    for (uint32_t base = 0; base < ns; base += 64) {
+      const uint32_t m = ns - base < 64 ? ns - base : 64;
+      if ((uint32_t)lane < m) st.nid[lane] = a.seeds[sb + base + lane];
+      __syncthreads();
+      qg_exact<PPL, NCH>(qlds, a, st.nid, st.nd, (int)m);
+      __syncthreads();
+      if ((uint32_t)lane < m) {
+        const uint32_t id = st.nid[lane];
+        visit(a.ht_log2, st, id, bitmap_mode, vis, epoch);
+        const uint64_t key = make_key(st.nd[lane], id);
+        if (ncq + lane < a.cq_cap) st.cq[ncq + lane] = key;
+        else spill[nspill + (ncq + lane - a.cq_cap)] = key;
+      }
+      __syncthreads();
+      for (uint32_t j = 0; j < m; j++) {
+        const float d = st.nd[j];
+        if (d <= a.radius) res_insert(st.res, nres, size, make_key(d, st.nid[j]));
+      }
+      if (ncq + m <= a.cq_cap) {
+        ncq += m;
+      } else {
+        nspill += ncq + m - a.cq_cap;
+        ncq = a.cq_cap;
+      }
+      nexact += m;
+      nvisited += m;
+      __syncthreads();
+      if (!bitmap_mode && nvisited > hlimit) {
+        ht_to_vis(a.ht_log2, st, vis, epoch);
+        bitmap_mode = true;
+        __syncthreads();
+      }
+    }
+    if (nres >= size) radius = key_dist(st.res[size - 1]);
+    float expr = __fmul_rn(a.coef, radius);
+
+    // ---- best-first loop over ADC distances (QuantizedGraph.h:220-268) ----
+    for (;;) {
+      uint64_t best = ~0ull;
+      uint32_t bidx = 0xffffffffu;
+      for (uint32_t i = lane; i < ncq; i += 64) {
+        const uint64_t key = st.cq[i];
+        if (key < best) { best = key; bidx = i; }
+      }
+      for (uint32_t i = lane; i < nspill; i += 64) {
+        const uint64_t key = spill[i];
+        if (key < best) { best = key; bidx = i | 0x80000000u; }
+      }
+      const uint64_t wbest = wave_min_u64(best);
+      if (wbest == ~0ull) break;
+      if (key_dist(wbest) > expr) break;
+      const uint64_t owner = ballot64(best == wbest);
+      const int olane = __ffsll((long long)owner) - 1;
+      bidx = __shfl(bidx, olane, 64);
+      if (lane == 0) {
+        if (bidx & 0x80000000u) spill[bidx & 0x7fffffffu] = spill[nspill - 1];
+        else st.cq[bidx] = st.cq[ncq - 1];
+      }
+      if (bidx & 0x80000000u) nspill--; else ncq--;
+      nexp++;
+
+      // neighbour ids (0-terminated fixed-stride row) and their ADC distances
+      const uint32_t target = key_id(wbest);
+      const uint32_t* nbr = a.qids + (uint64_t)target * a.id_stride;
+      uint32_t deg = 0;
+      for (uint32_t j = 0; j < a.id_stride; j += 64) {
+        const uint32_t id = j + lane < a.id_stride ? nbr[j + lane] : 0u;
+        st.nid[j + lane] = id;
+        deg += (uint32_t)__popcll(ballot64(id != 0u));
+      }
+      adc_node<PPL>(L, a.qcodes + (uint64_t)target * a.code_stride, a.Me, deg, scale, toff, st.nd);
+      __syncthreads();
+      nadc += deg;
+      nblk += deg == 0 ? 0 : (deg - 1) / 16 + 1;
+
+      // accept in neighbour order (QuantizedGraph.h:241-266): ids of one list
+      // are distinct, so the visited test of a chunk runs in parallel and only
+      // the radius bookkeeping is sequential.
+      for (uint32_t base = 0; base < deg; base += 64) {
+        const uint32_t i = base + lane;
+        const bool in = i < deg && st.nd[i] <= expr;
+        const bool seen = in && visited_test(a.ht_log2, st.ht, st.nid[i], bitmap_mode, vis, epoch);
+        uint64_t cand = ballot64(in && !seen);
+        uint64_t acc = 0;
+        while (cand) {
+          const int j = __ffsll((long long)cand) - 1;
+          cand &= cand - 1;
+          const float d = st.nd[base + j];
+          if (!(d <= expr)) continue;
+          acc |= 1ull << j;
+          const uint64_t key = make_key(d, st.nid[base + j]);
+          if (ncq >= a.cq_cap) {
+            ncq = compact(st.cq, ncq, expr);
+            if (nspill) nspill = compact(spill, nspill, expr);
+          }
+          if (ncq < a.cq_cap) {
+            if (lane == 0) st.cq[ncq] = key;
+            ncq++;
+          } else {
+            if (nspill >= a.spill_cap) {
+              if (lane == 0) atomicOr(a.error, 1);
+            } else {
+              if (lane == 0) spill[nspill] = key;
+              nspill++;
+            }
+          }
+          if (d <= radius) {
+            res_insert(st.res, nres, size, key);
+            if (nres >= size) {
+              radius = key_dist(st.res[size - 1]);
+              expr = __fmul_rn(a.coef, radius);
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+        // mark the accepted ids
+        if ((acc >> lane) & 1ull) visit(a.ht_log2, st, st.nid[i], bitmap_mode, vis, epoch);
+        const uint32_t na = (uint32_t)__popcll(acc);
+        nacc += na;
+        nvisited += na;
+        if (ncq + nspill > maxq) maxq = ncq + nspill;
+        __syncthreads();
+        if (!bitmap_mode && nvisited > hlimit) {
+          ht_to_vis(a.ht_log2, st, vis, epoch);
+          bitmap_mode = true;
+          __syncthreads();
+        }
+      }
+    }
+
+    // ---- results (QuantizedGraph.h:270-299) ------------------------------
+    uint32_t nout = nres;
+    if (a.rerank) {
+      // exact distances of the expanded result set, sorted by (distance, id),
+      // resized to k (padding {0, 0} when short)
+      for (uint32_t base = 0; base < nres; base += 64) {
+        const uint32_t m = nres - base < 64 ? nres - base : 64;
+        if ((uint32_t)lane < m) st.nid[lane] = key_id(st.res[base + lane]);
+        __syncthreads();
+        qg_exact<PPL, NCH>(qlds, a, st.nid, st.nd, (int)m);
+        __syncthreads();
+        if ((uint32_t)lane < m) rr[base + lane] = make_key(st.nd[lane], st.nid[lane]);
+        __syncthreads();
+      }
+      nexact += nres;
+      // rank sort: position of each key = number of smaller keys (distinct ids)
+      for (uint32_t i = lane; i < nres; i += 64) {
+        const uint64_t key = rr[i];
+        uint32_t pos = 0;
+        for (uint32_t j = 0; j < nres; j++) pos += rr[j] < key ? 1u : 0u;
+        st.res[pos] = key;
+      }
+      __syncthreads();
+      for (uint32_t i = lane; i < a.k; i += 64) {
+        a.out_ids[(uint64_t)qi * a.k + i] = i < nres ? key_id(st.res[i]) : 0u;
+        a.out_dists[(uint64_t)qi * a.k + i] = i < nres ? key_dist(st.res[i]) : 0.0f;
+      }
+      nout = a.k;
+    } else {
+      for (uint32_t i = lane; i < nres; i += 64) {
+        a.out_ids[(uint64_t)qi * a.k + i] = key_id(st.res[i]);
+        a.out_dists[(uint64_t)qi * a.k + i] = key_dist(st.res[i]);
+      }
+    }
+    if (lane == 0) {
+      a.out_n[qi] = nout;
+      if (a.counters) {
+        uint64_t* c = a.counters + (uint64_t)qi * 8;
+        c[0] = nadc;
+        c[1] = nacc;
+        c[2] = nexp;
+        c[3] = nexact;
+        c[4] = nblk;
+        c[5] = maxq;
+        c[6] = (bitmap_mode && use_hash) ? 1 : 0;
+        c[7] = 0;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers.
+// ---------------------------------------------------------------------------
+static int ppl_of(uint32_t Me) {
+  const uint32_t pairs = Me / 2;
+  if (pairs <= 64) return 1;
+  if (pairs <= 128) return 2;
+  if (pairs <= 256) return 4;  // Me <= 512 keeps the packed u16 sums exact
+  return 0;
+}
+
+hipError_t launch_qg_lut(const QgLutArgs& a, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = (size_t)a.M * 16 * sizeof(float);
+  const uint32_t blocks = a.nq < 16384 ? a.nq : 16384;
+  hipLaunchKernelGGL(ngt_qg_lut_kernel, dim3(blocks), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_qg_build(const QgBuildArgs& a, hipStream_t s) {
+  if (a.nrows == 0) return hipSuccess;
+  uint64_t blocks = ((uint64_t)a.nrows + 3) / 4;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(ngt_qg_build_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_qg_adc(const QgAdcArgs& a, hipStream_t s) {
+  if (a.npairs == 0) return hipSuccess;
+  const size_t lds = (size_t)((a.id_stride + 63) & ~63u) * sizeof(float);
+  const uint32_t blocks = a.npairs < 65536 ? (uint32_t)a.npairs : 65536;
+  switch (ppl_of(a.Me)) {
+    case 1: hipLaunchKernelGGL((ngt_qg_adc_kernel<1>), dim3(blocks), dim3(64), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((ngt_qg_adc_kernel<2>), dim3(blocks), dim3(64), lds, s, a); break;
+    case 4: hipLaunchKernelGGL((ngt_qg_adc_kernel<4>), dim3(blocks), dim3(64), lds, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+size_t qg_search_lds_bytes(const QgSearchArgs& a) {
+  size_t b = (a.ht_log2 ? ((size_t)4 << a.ht_log2) : 0) + (size_t)8 * a.cq_cap;
+  b += 2 * (((size_t)8 * (a.size + 1) + 15) & ~(size_t)15);
+  const uint32_t nstage = a.id_stride > a.size ? a.id_stride : a.size;
+  b += (size_t)8 * ((nstage + 63) & ~63u);
+  b += (size_t)a.dp * 4;
+  return b;
+}
+
+hipError_t launch_qg_search(const QgSearchArgs& a, uint32_t slots, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = qg_search_lds_bytes(a);
+#define L_QG(P, N) hipLaunchKernelGGL((ngt_qg_search_kernel<P, N>), dim3(slots), dim3(64), lds, s, a)
+  const int ppl = ppl_of(a.Me);
+  if (a.dp == 128) {
+    switch (ppl) {
+      case 1: L_QG(1, 8); break;
+      case 2: L_QG(2, 8); break;
+      case 4: L_QG(4, 8); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (ppl) {
+      case 1: L_QG(1, 0); break;
+      case 2: L_QG(2, 0); break;
+      case 4: L_QG(4, 0); break;
+      default: return hipErrorInvalidValue;
+    }
+  }
+#undef L_QG
+  return hipGetLastError();
+}
+
+}  // namespace ngt_amd

@@ -27,6 +27,7 @@
 
 #include "ngt_device.h"
 #include "ngt_kernels.h"
+#include "search_common.h"
 
 namespace ngt_amd {
 
@@ -79,35 +80,6 @@ struct GlibcRand {
   }
 };
 
-template <typename T>
-__device__ __forceinline__ const T* row_ptr(const uint8_t* rows, uint64_t row_bytes, uint32_t id) {
-  return reinterpret_cast<const T*>(rows + (uint64_t)id * row_bytes);
-}
-
-// Copy a padded query row (dp elements) into LDS with 16-byte stores.
-template <typename T>
-__device__ __forceinline__ void load_query(T* qlds, const uint8_t* src, int dp) {
-  const int n16 = (dp * (int)sizeof(T)) >> 4;
-  const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4* d = reinterpret_cast<uint4*>(qlds);
-  for (int i = lane_id(); i < n16; i += 64) d[i] = s[i];
-}
-
-// Distances for `m` candidate ids staged in LDS; 16 rows per wave step,
-// 4 lanes per row.  Results land in dists[0..m).
-template <int M, typename T>
-__device__ __forceinline__ void eval_batch(const T* qlds, const uint8_t* rows, uint64_t row_bytes,
-                                           int dp, const uint32_t* ids, float* dists, int m) {
-  const int lane = lane_id();
-  const int g = lane & 3;
-  for (int r0 = 0; r0 < m; r0 += 16) {
-    const int r = r0 + (lane >> 2);
-    if (r < m) {
-      const float d = quad_distance<M, T>(qlds, row_ptr<T>(rows, row_bytes, ids[r]), dp, g);
-      if (g == 0) dists[r] = d;
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Batched comparator.  pair i: (query qidx[i], object oid[i]) -> out[i].
@@ -184,146 +156,6 @@ __global__ void __launch_bounds__(64) ngt_tree_seed_kernel(TreeSeedArgs a) {
 // ---------------------------------------------------------------------------
 // Graph search.
 // ---------------------------------------------------------------------------
-struct SearchState {
-  uint32_t* ht;      // visited hash (LDS)
-  uint64_t* cq;      // unchecked keys (LDS)
-  uint64_t* res;     // sorted results (LDS)
-  uint32_t* nid;     // staged candidate ids (LDS, 64)
-  float* nd;         // staged distances (LDS, 64)
-};
-
-__device__ __forceinline__ uint32_t ht_hash(uint32_t id, uint32_t shift) {
-  return (id * 0x9E3779B1u) >> shift;
-}
-
-// Insert `id` into the visited set; true if it was not present.  Two exact
-// forms: an LDS open-addressing hash (small searches), or the slot's HBM
-// byte array of query epochs (vis[id] == epoch <=> visited).  The byte form
-// needs no read-modify-write: the test is a plain L2 load (sc1, so this CU's
-// L1 cannot serve a stale line) and the mark is a plain byte store -- no
-// scattered device atomics (MI355X_MICROARCH.md, Global float atomics: 64 lanes
-// in 64 rows run ~17x slower than contiguous).
-__device__ __forceinline__ bool visit(const SearchArgs& a, SearchState& st, uint32_t id,
-                                      bool vis_mode, uint8_t* vis, uint32_t epoch) {
-  if (vis_mode) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
-    const uint32_t word = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t old = (word >> (8 * (id & 3))) & 0xffu;
-    if (old == epoch) return false;
-    vis[id] = (uint8_t)epoch;
-    return true;
-  }
-  const uint32_t mask = (1u << a.ht_log2) - 1;
-  uint32_t h = ht_hash(id, 32 - a.ht_log2);
-  for (;;) {
-    const uint32_t old = atomicCAS(st.ht + h, 0u, id);
-    if (old == 0u) return true;
-    if (old == id) return false;
-    h = (h + 1) & mask;
-  }
-}
-
-// Move the LDS hash contents into the slot's epoch array (exact overflow path).
-__device__ void ht_to_vis(const SearchArgs& a, SearchState& st, uint8_t* vis, uint32_t epoch) {
-  const uint32_t n = 1u << a.ht_log2;
-  for (uint32_t i = lane_id(); i < n; i += 64) {
-    const uint32_t id = st.ht[i];
-    if (id) vis[id] = (uint8_t)epoch;
-  }
-  __threadfence_block();
-}
-
-// Sorted insert of `key` into res[0..nres) keeping at most k entries.
-__device__ __forceinline__ void res_insert(uint64_t* res, uint32_t& nres, uint32_t k, uint64_t key) {
-  const int lane = lane_id();
-  uint32_t lt = 0;
-  for (uint32_t i = lane; i < nres; i += 64) lt += res[i] < key ? 1u : 0u;
-  const uint32_t pos = wave_sum_u32(lt);
-  if (pos >= k) return;
-  const uint32_t last = nres < k - 1 ? nres : k - 1;  // [pos, last) moves up one
-  if (last > pos) {
-    for (int c = (int)((last - 1) >> 6); c >= (int)(pos >> 6); c--) {
-      const uint32_t i = (uint32_t)c * 64 + lane;
-      uint64_t v = 0;
-      const bool mv = i >= pos && i < last;
-      if (mv) v = res[i];
-      __builtin_amdgcn_wave_barrier();
-      if (mv) res[i + 1] = v;
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  if (lane == 0) res[pos] = key;
-  __builtin_amdgcn_wave_barrier();
-  nres = nres + 1 < k ? nres + 1 : k;
-}
-
-// Drop unchecked entries farther than expR (they can never be expanded).
-__device__ __forceinline__ uint32_t compact(uint64_t* v, uint32_t n, float expr) {
-  const int lane = lane_id();
-  uint32_t out = 0;
-  for (uint32_t b = 0; b < n; b += 64) {
-    const uint32_t i = b + lane;
-    uint64_t key = i < n ? v[i] : ~0ull;
-    const bool keep = i < n && key_dist(key) <= expr;
-    const uint64_t mask = ballot64(keep);
-    __builtin_amdgcn_wave_barrier();
-    if (keep) v[out + mbcnt(mask)] = key;
-    __builtin_amdgcn_wave_barrier();
-    out += (uint32_t)__popcll(mask);
-  }
-  return out;
-}
-
-// L2 over float rows with a compile-time chunk count (dp = 16 * NCH): the
-// query lives in registers and the loads of two 16-row groups (32 rows,
-// 16 KiB at dp = 128) are all issued before the first FMA, so one batch costs
-// one memory round trip.  Same quad mapping and folds as dist_f32<kL2>, hence
-// bit-identical results.  Out-of-range lanes read the dummy row 0.
-template <int NCH>
-__device__ __forceinline__ float l2_fold_rows(const float4* qq, const float4 (&v)[NCH]) {
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int i = 0; i < NCH; i++) {
-    const float4 q = qq[4 * i];  // query stays in LDS: ds_read_b128, saves 4*NCH VGPRs
-    const float vx = q.x - v[i].x, vy = q.y - v[i].y, vz = q.z - v[i].z, vw = q.w - v[i].w;
-    acc.x = __builtin_fmaf(vx, vx, acc.x);
-    acc.y = __builtin_fmaf(vy, vy, acc.y);
-    acc.z = __builtin_fmaf(vz, vz, acc.z);
-    acc.w = __builtin_fmaf(vw, vw, acc.w);
-  }
-  return (float)sqrt((double)fold16(acc));
-}
-
-// G = 16-row groups whose loads are in flight together (G=1: 16 rows / 8 KiB
-// per round trip at dp=128, low VGPR count, more resident waves; G=2: 32 rows).
-template <int NCH, int G>
-__device__ __forceinline__ void eval_l2f_fast(const float* qlds, const uint8_t* rows, uint64_t row_bytes,
-                                              const uint32_t* ids, float* dists, int m) {
-  const int lane = lane_id();
-  const int g = lane & 3, rs = lane >> 2;
-  const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
-  for (int r0 = 0; r0 < m; r0 += 16 * G) {
-    float4 v[G][NCH];
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-      if (j == 0 || r0 + 16 * j < m) {
-        const int r = r0 + 16 * j + rs;
-        const uint32_t id = r < m ? ids[r] : 0u;
-        const float4* x = reinterpret_cast<const float4*>(rows + (uint64_t)id * row_bytes) + g;
-#pragma unroll
-        for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-      if (j == 0 || r0 + 16 * j < m) {
-        const int r = r0 + 16 * j + rs;
-        const float d = l2_fold_rows<NCH>(qq, v[j]);
-        if (g == 0 && r < m) dists[r] = d;
-      }
-    }
-  }
-}
 
 template <int M, typename T, int NCH, int G>
 __device__ __forceinline__ void eval_any(const T* qlds, const SearchArgs& a, const uint32_t* ids, float* dists,
@@ -403,7 +235,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
       if ((uint32_t)lane < m) {
         const uint32_t id = st.nid[lane];
         const uint64_t key = make_key(st.nd[lane], id);
-        visit(a, st, id, bitmap_mode, vis, epoch);
+        visit(a.ht_log2, st, id, bitmap_mode, vis, epoch);
         if (ncq + lane < a.cq_cap) st.cq[ncq + lane] = key;
         else spill[nspill + (ncq + lane - a.cq_cap)] = key;
       }
@@ -423,7 +255,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
       nvisited += m;
       __syncthreads();
       if (!bitmap_mode && nvisited > hlimit) {
-        ht_to_vis(a, st, vis, epoch);
+        ht_to_vis(a.ht_log2, st, vis, epoch);
         bitmap_mode = true;
         __syncthreads();
       }
@@ -479,7 +311,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
         if ((uint32_t)lane < cnt) id = padded ? a.adj[eb + base + lane] : a.edges[eb + base + lane];
         const uint64_t vmask = ballot64(id != 0u);
         nedge += (uint64_t)__popcll(vmask);
-        const bool fresh = id != 0u && visit(a, st, id, bitmap_mode, vis, epoch);
+        const bool fresh = id != 0u && visit(a.ht_log2, st, id, bitmap_mode, vis, epoch);
         const uint64_t fmask = ballot64(fresh);
         const uint32_t m = (uint32_t)__popcll(fmask);
         if (fresh) st.nid[mbcnt(fmask)] = id;
@@ -529,7 +361,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
           __syncthreads();
           // exact overflow of the visited set into the HBM bitmap
           if (!bitmap_mode && nvisited > hlimit) {
-            ht_to_vis(a, st, vis, epoch);
+            ht_to_vis(a.ht_log2, st, vis, epoch);
             bitmap_mode = true;
             __syncthreads();
           }

@@ -12,7 +12,7 @@ from ctypes import byref, c_void_p
 import numpy as np
 
 from . import NativeError, lib
-from ._sigs import SearchParams
+from ._sigs import QgSearchParams, SearchParams
 
 DISTANCE = {
     "l1": 0, "l2": 1, "hamming": 2, "angle": 3, "cosine": 4, "normalized_angle": 5,
@@ -159,6 +159,81 @@ class DeviceIndex(object):
         _chk(self.L.ngt_amd_distances(self.h, q.ctypes.data, q.shape[0], qidx.ctypes.data, oid.ctypes.data,
                                       len(oid), out.ctypes.data))
         return out
+
+    # ---- NGTQG quantized graph (L2 float) ---------------------------------
+    def qg_set_quantizer(self, global_centroid, local):
+        """global_centroid: [dim]; local: [M, 16, dsub] (local ids 1..16)."""
+        g = np.ascontiguousarray(np.asarray(global_centroid, np.float32)[:self.dim])
+        loc = np.ascontiguousarray(local, dtype=np.float32)
+        M, _, dsub = loc.shape
+        _chk(self.L.ngt_amd_qg_set_quantizer(self.h, g.ctypes.data, loc.ctypes.data, M, dsub))
+        self.qg_M = M
+        self.qg_Me = (M + 1) // 2 * 2
+
+    def qg_build_graph(self, local_codes, max_edges=128):
+        """local_codes: [nrows, M] localID - 1 (0..15) of every object."""
+        c = np.ascontiguousarray(local_codes, dtype=np.uint8)
+        _chk(self.L.ngt_amd_qg_build_graph(self.h, c.ctypes.data, max_edges))
+
+    def qg_set_graph(self, qoff, qids, code_off, codes):
+        qoff = np.ascontiguousarray(qoff, dtype=np.uint64)
+        qids = np.ascontiguousarray(qids if len(qids) else np.zeros(1), dtype=np.uint32)
+        code_off = np.ascontiguousarray(code_off, dtype=np.uint64)
+        codes = np.ascontiguousarray(codes if len(codes) else np.zeros(1), dtype=np.uint8)
+        _chk(self.L.ngt_amd_qg_set_graph(self.h, qoff.ctypes.data, qids.ctypes.data, code_off.ctypes.data,
+                                         codes.ctypes.data))
+
+    def qg_max_degree(self):
+        return int(self.L.ngt_amd_qg_max_degree(self.h))
+
+    def qg_lut(self, queries):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        nq = q.shape[0]
+        lut = np.zeros((nq, self.qg_Me * 16), np.uint8)
+        sc = np.zeros(nq, np.float32)
+        to = np.zeros(nq, np.float32)
+        _chk(self.L.ngt_amd_qg_lut(self.h, q.ctypes.data, nq, lut.ctypes.data, sc.ctypes.data, to.ctypes.data))
+        return lut, sc, to
+
+    def qg_adc(self, lut, scale, total_offset, qidx, nodes):
+        lut = np.ascontiguousarray(lut, dtype=np.uint8)
+        sc = np.ascontiguousarray(scale, dtype=np.float32)
+        to = np.ascontiguousarray(total_offset, dtype=np.float32)
+        qidx = np.ascontiguousarray(qidx, dtype=np.uint32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        md = self.qg_max_degree()
+        out = np.zeros((len(nodes), md), np.float32)
+        n = np.zeros(len(nodes), np.uint32)
+        _chk(self.L.ngt_amd_qg_adc(self.h, lut.ctypes.data, sc.ctypes.data, to.ctypes.data, lut.shape[0],
+                                   qidx.ctypes.data, nodes.ctypes.data, len(nodes), out.ctypes.data, n.ctypes.data))
+        return out, n
+
+    def qg_search(self, queries, k=20, epsilon=0.03, result_expansion=3.0, radius=-1.0, seed_mode=SEED_TREE,
+                  seeds=None, counters=True, visited_hash_log2=0):
+        """NGTQG::Index::search for a batch; defaults of ngtqg_initialize_query."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        nq = q.shape[0]
+        prm = QgSearchParams(k, epsilon, result_expansion, radius, seed_mode, visited_hash_log2)
+        ids = np.zeros((nq, k), np.uint32)
+        ds = np.zeros((nq, k), np.float32)
+        n = np.zeros(nq, np.uint32)
+        cnt = np.zeros((nq, COUNTERS), np.uint64) if counters else None
+        sp = so = None
+        if seed_mode == SEED_GIVEN:
+            so = np.zeros(nq + 1, np.uint64)
+            so[1:] = np.cumsum([len(s) for s in seeds])
+            sp = np.ascontiguousarray(np.concatenate([np.asarray(s, np.uint32) for s in seeds])
+                                      if so[-1] else np.zeros(1, np.uint32))
+        _chk(self.L.ngt_amd_qg_search(self.h, byref(prm), q.ctypes.data, nq, _ptr(sp), _ptr(so), ids.ctypes.data,
+                                      ds.ctypes.data, n.ctypes.data, _ptr(cnt)))
+        return ids, ds, n, cnt
+
+    def qg_search_device(self, d_queries, query_bytes, nq, d_ids, d_dists, d_n, d_counters=None, k=20,
+                         epsilon=0.03, result_expansion=3.0, radius=-1.0, seed_mode=SEED_TREE, d_seeds=None,
+                         d_seed_off=None, stream=None, visited_hash_log2=0):
+        prm = QgSearchParams(k, epsilon, result_expansion, radius, seed_mode, visited_hash_log2)
+        _chk(self.L.ngt_amd_qg_search_device(self.h, byref(prm), d_queries, query_bytes, nq, d_seeds, d_seed_off,
+                                             d_ids, d_dists, d_n, d_counters, stream))
 
     def close(self):
         if getattr(self, "h", None):

@@ -1,0 +1,177 @@
+"""GPU parity of the NGTQG path (qg_kernels.hip through the C ABI) against the
+reference's own outputs (tests/golden/*_qg, made by make_qg_goldens.py from
+the reference library) and against the CPU restatement (oracle/).
+
+Bar: LUT bytes, scale and totalOffset bit-exact; ADC distances bit-exact;
+NGTQG::Index::search ids and float distances identical for every
+(k, epsilon, result_expansion) the fixtures hold."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import ngt_files as F
+import oracle_py as O
+from ngt_amd.device import SEED_GIVEN, SEED_TREE, DeviceIndex
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = {"c1_qg": ("c1_onng", 128, 128), "d20_qg": ("d20_qg", 20, 64)}
+_CACHE = {}
+
+
+def state(name):
+    if name not in _CACHE:
+        src, dim, maxe = CASES[name]
+        offs, ids, _ = F.read_grp(os.path.join(GOLD, src, "grp"))
+        qg = F.read_qg(os.path.join(GOLD, name), offs, ids, maxe)
+        rows, valid = F.read_obj(os.path.join(GOLD, src, "obj"), dim, np.float32)
+        tree = F.read_tre(os.path.join(GOLD, src, "tre"), dim, np.float32)
+        prop = F.read_prf(os.path.join(GOLD, src, "prf"))
+        z = dict(np.load(os.path.join(GOLD, name, "goldens.npz")))
+        meta = json.load(open(os.path.join(GOLD, name, "meta.json")))
+        _CACHE[name] = (qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe)
+    return _CACHE[name]
+
+
+def local_codes(qg, nrows):
+    """[nrows, M] localID - 1 from qg/ivt (rows without an entry: 0)."""
+    lid = qg["local_ids"]
+    out = np.zeros((nrows, qg["M"]), np.uint8)
+    n = min(nrows, lid.shape[0])
+    out[:n] = (lid[:n].astype(np.int32) - 1).clip(0, 15).astype(np.uint8)
+    return out
+
+
+def device_qg(name, build="device"):
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state(name)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows, valid)
+    ix.set_graph(offs, ids)
+    ix.set_tree(tree)
+    ix.set_search_property(int(prop["EdgeSizeForSearch"]), int(prop["DynamicEdgeSizeBase"]),
+                           int(prop["DynamicEdgeSizeRate"]), int(prop["SeedSize"]), 0)
+    ix.qg_set_quantizer(qg["global"], qg["local"][:, 1:17, :])
+    if build == "device":
+        ix.qg_build_graph(local_codes(qg, rows.shape[0]), maxe)
+    else:
+        ix.qg_set_graph(qg["qoff"], qg["qids"], qg["code_off"], qg["codes"])
+    return ix
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_qg_lut_bit_exact_vs_reference(name):
+    qg, *_, z, meta, dim, maxe = state(name)
+    ix = device_qg(name)
+    qs = z["queries"].astype(np.float32)
+    lut, sc, to = ix.qg_lut(qs)
+    for qi in range(len(qs)):
+        assert np.array_equal(lut[qi], z["lut"][qi]), qi
+    assert np.array_equal(sc.view(np.uint32), z["scale"].astype(np.float32).view(np.uint32))
+    assert np.array_equal(to.view(np.uint32), z["total_offset"].astype(np.float32).view(np.uint32))
+    ix.close()
+
+
+@pytest.mark.parametrize("build", ["device", "file"])
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_qg_adc_bit_exact_vs_reference(name, build):
+    """Device-built quantized graph (construct) and the host-packed one
+    (deserialize) both give the reference's ADC distances."""
+    qg, *_, z, meta, dim, maxe = state(name)
+    ix = device_qg(name, build)
+    nodes = np.asarray(z["nodes"], np.uint32)
+    nq = len(z["queries"])
+    qidx = np.repeat(np.arange(nq, dtype=np.uint32), len(nodes))
+    nn = np.tile(nodes, nq)
+    out, n = ix.qg_adc(z["lut"], z["scale"], z["total_offset"], qidx, nn)
+    for qi in range(nq):
+        got = np.concatenate([out[qi * len(nodes) + j, :n[qi * len(nodes) + j]] for j in range(len(nodes))])
+        assert np.array_equal(got.view(np.uint32), z["adc"][qi].view(np.uint32)), qi
+    ix.close()
+
+
+def _params(meta):
+    for p in meta["params"]:
+        k, eps, exp = p.split(":")
+        yield p.replace(":", "_"), int(k), float(eps), float(exp)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_qg_search_matches_reference(name):
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state(name)
+    ix = device_qg(name)
+    qs = z["queries"].astype(np.float32)
+    for key, k, eps, exp in _params(meta):
+        gi, gd, gn, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_TREE)
+        for qi in range(len(qs)):
+            n = int(z["n_" + key][qi])
+            assert int(gn[qi]) == n, (key, qi)
+            assert list(gi[qi, :n]) == list(z["ids_" + key][qi][:n]), (key, qi)
+            assert np.array_equal(gd[qi, :n].view(np.uint32), z["dist_" + key][qi][:n].view(np.uint32)), (key, qi)
+    ix.close()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_qg_search_counters_match_oracle(name):
+    """Same traversal as the restatement: ADC count, accepted, expansions and
+    exact distances agree query by query."""
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state(name)
+    ix = device_qg(name)
+    qs = z["queries"].astype(np.float32)
+    for k, eps, exp in [(10, 0.05, 3.0), (10, 0.1, 0.5)]:
+        gi, gd, gn, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_TREE)
+        for qi, q in enumerate(qs):
+            qq = np.zeros(rows.shape[1], np.float32)
+            qq[:len(q)] = q
+            seeds, _, _ = O.tree_seeds("l2", tree, qq, k, int(prop["SeedSize"]))
+            oid, od, ocnt = O.qg_search(qg, rows, qq, seeds, k, np.float32(eps), np.float32(exp))
+            assert list(gi[qi, :gn[qi]]) == list(oid), (k, eps, exp, qi)
+            assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32))
+            assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt], (k, eps, exp, qi)
+    ix.close()
+
+
+@pytest.mark.parametrize("ht,cq", [("8", "64"), ("bitmap", "64"), ("9", "1024")])
+def test_qg_overflow_paths_exact(monkeypatch, ht, cq):
+    """Tiny LDS capacities force the visited hash -> HBM epochs and the
+    unchecked array -> HBM spill; results must not change."""
+    if ht != "bitmap":
+        monkeypatch.setenv("NGT_AMD_HT_LOG2", ht)
+    monkeypatch.setenv("NGT_AMD_CQ_CAP", cq)
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("c1_qg")
+    ix = device_qg("c1_qg")
+    rng = np.random.default_rng(5)
+    qs = z["queries"].astype(np.float32)
+    seeds = [rng.choice(np.arange(1, rows.shape[0]), 10, replace=False).astype(np.uint32) for _ in qs]
+    for eps, exp in [(0.3, 3.0), (0.6, 2.0)]:
+        gi, gd, gn, cnt = ix.qg_search(qs, k=20, epsilon=eps, result_expansion=exp, seed_mode=SEED_GIVEN,
+                                       seeds=seeds, visited_hash_log2=-1 if ht == "bitmap" else 0)
+        for qi, q in enumerate(qs):
+            oid, od, ocnt = O.qg_search(qg, rows, q, seeds[qi], 20, np.float32(eps), np.float32(exp))
+            assert list(gi[qi, :gn[qi]]) == list(oid), (eps, qi)
+            assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32))
+            assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt]
+    ix.close()
+
+
+def test_qg_edge_cases():
+    """Seeds-only searches, result_expansion < 1 (ADC distances returned),
+    a tiny radius and k beyond the reachable set pad like the reference."""
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("d20_qg")
+    ix = device_qg("d20_qg")
+    qs = z["queries"].astype(np.float32)[:4]
+    seeds = [np.array([1, 2, 3], np.uint32), np.array([], np.uint32), np.array([5], np.uint32),
+             np.array([7, 8], np.uint32)]
+    for k, eps, exp, rad in [(5, 0.1, 0.5, -1.0), (300, 0.02, 1.0, -1.0), (10, 0.1, 3.0, 0.05),
+                             (7, 0.0, 1.5, -1.0)]:
+        gi, gd, gn, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, radius=rad,
+                                       seed_mode=SEED_GIVEN, seeds=seeds)
+        for qi, q in enumerate(qs):
+            r = np.float32(3.402823466e38) if rad < 0 else np.float32(rad)
+            oid, od, ocnt = O.qg_search(qg, rows, q, seeds[qi], k, np.float32(eps), np.float32(exp), radius=r)
+            assert int(gn[qi]) == len(oid), (k, eps, exp, rad, qi)
+            assert list(gi[qi, :gn[qi]]) == list(oid), (k, eps, exp, rad, qi)
+            assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32))
+    ix.close()
