@@ -14,6 +14,15 @@ class QgSearchParams(Structure):
                 ("seed_mode", c_int32), ("visited_hash_log2", c_int32)]
 
 
+class NGTQGQuery(Structure):
+    _fields_ = [("query", POINTER(c_float)), ("size", c_size_t), ("epsilon", c_float),
+                ("result_expansion", c_float), ("radius", c_float)]
+
+
+class NGTQGQuantizationParameters(Structure):
+    _fields_ = [("dimension_of_subvector", c_float), ("max_number_of_edges", c_size_t)]
+
+
 class ObjectDistance(Structure):
     _fields_ = [("id", c_uint), ("distance", c_float)]
 
@@ -126,6 +135,15 @@ def declare(L):
         "ngt_batch_linear_search_index": (c_bool, [vp, f32p, c_uint32, c_int32, c_size_t, u32p, f32p, u32p,
                                                    vp]),
         "ngt_get_last_search_counters": (c_bool, [vp, u64p, vp]),
+        # ---- include/NGT/NGTQ/Capi.h
+        "ngtqg_open_index": (vp, [c_char_p, vp]),
+        "ngtqg_close_index": (None, [vp]),
+        "ngtqg_initialize_quantization_parameters": (None, [POINTER(NGTQGQuantizationParameters)]),
+        "ngtqg_quantize": (c_bool, [c_char_p, NGTQGQuantizationParameters, vp]),
+        "ngtqg_initialize_query": (None, [POINTER(NGTQGQuery)]),
+        "ngtqg_search_index": (c_bool, [vp, NGTQGQuery, vp, vp]),
+        "ngtqg_batch_search_index": (c_bool, [vp, f32p, c_uint32, c_int32, c_size_t, c_float, c_float, c_float,
+                                              u32p, f32p, u32p, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

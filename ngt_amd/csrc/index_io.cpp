@@ -378,3 +378,118 @@ std::string save_index(const std::string& dir, HostIndex& ix) {
 }
 
 }  // namespace ngt_amd
+
+namespace ngt_amd {
+
+// obj file of 32-bit float rows of `dim` elements (slot 0 = dummy).
+static std::string read_float_obj(const std::string& path, uint32_t dim, std::vector<float>& rows,
+                                  uint64_t& n) {
+  Reader r;
+  if (!r.open(path)) return "cannot open " + path;
+  n = r.get<uint64_t>();
+  rows.assign(n * dim, 0.f);
+  for (uint64_t i = 0; i < n && r.ok; i++) {
+    char t = r.get<char>();
+    if (t == '+') r.bytes(rows.data() + i * dim, (size_t)dim * 4);
+    else if (t != '-') return "corrupt obj file " + path;
+  }
+  if (!r.ok) return "truncated obj file " + path;
+  return "";
+}
+
+std::string load_qg(const std::string& dir, uint64_t nrows, HostQuantizer& q) {
+  const std::string qd = dir + "/qg";
+  HostProperty p;
+  {
+    std::ifstream f(qd + "/prf");
+    if (!f) return "cannot open " + qd + "/prf (not an NGTQG index: run ngtqg quantize)";
+    std::string line;
+    while (std::getline(f, line)) {
+      size_t t = line.find('\t');
+      if (t != std::string::npos) p.kv[line.substr(0, t)] = line.substr(t + 1);
+    }
+  }
+  const long dim = getl(p.kv, "Dimension", 0), M = getl(p.kv, "LocalDivisionNo", 0);
+  if (dim <= 0 || M <= 0 || dim % M != 0) return "invalid Dimension/LocalDivisionNo in " + qd + "/prf";
+  if (getl(p.kv, "LocalIDByteSize", 2) != 2) return "unsupported LocalIDByteSize in " + qd + "/prf";
+  q.dim = (uint32_t)dim;
+  q.M = (uint32_t)M;
+  q.dsub = (uint32_t)(dim / M);
+  // global codebook: centroid 1 (QuantizedGraph.h:397-399 inserts the zero vector)
+  {
+    std::vector<float> rows;
+    uint64_t n = 0;
+    std::string e = read_float_obj(qd + "/global/obj", q.dim, rows, n);
+    if (!e.empty()) return e;
+    if (n < 2) return "empty global codebook";
+    q.global.assign(rows.begin() + q.dim, rows.begin() + 2 * q.dim);
+  }
+  // local codebooks: local-m/obj, ids 1..16
+  q.local.assign((size_t)q.M * 16 * q.dsub, 0.f);
+  for (uint32_t m = 0; m < q.M; m++) {
+    std::vector<float> rows;
+    uint64_t n = 0;
+    std::string e = read_float_obj(qd + "/local-" + std::to_string(m) + "/obj", q.dsub, rows, n);
+    if (!e.empty()) return e;
+    for (uint64_t c = 1; c < n && c <= 16; c++)
+      std::copy(rows.begin() + c * q.dsub, rows.begin() + (c + 1) * q.dsub,
+                q.local.begin() + ((size_t)m * 16 + c - 1) * q.dsub);
+  }
+  // ivt: Repository<InvertedIndexEntry<uint16_t>> (NGTQ/Quantizer.h:105-132) ->
+  // per object the M local ids (1..16); stored as localID - 1
+  q.codes.assign(nrows * q.M, 0);
+  {
+    Reader r;
+    if (!r.open(qd + "/ivt")) return "cannot open " + qd + "/ivt";
+    uint64_t n = r.get<uint64_t>();
+    for (uint64_t s = 0; s < n && r.ok; s++) {
+      char t = r.get<char>();
+      if (t == '-') continue;
+      if (t != '+') return "corrupt ivt";
+      uint32_t sz = r.get<uint32_t>();
+      uint16_t nids = r.get<uint16_t>();
+      const size_t pad = ((size_t)(nids * 2 - 1) / 4 + 1) * 4;
+      std::vector<uint16_t> lid(pad / 2);
+      for (uint32_t i = 0; i < sz && r.ok; i++) {
+        uint32_t id = r.get<uint32_t>();
+        r.bytes(lid.data(), pad);
+        if (id >= nrows) return "ivt object id out of range";
+        for (uint32_t m = 0; m < q.M && m < nids; m++) {
+          if (lid[m] < 1 || lid[m] > 16) return "invalid local centroid id in ivt";
+          q.codes[(size_t)id * q.M + m] = (uint8_t)(lid[m] - 1);
+        }
+      }
+    }
+    if (!r.ok) return "truncated ivt";
+  }
+  // qg/grp, if saved (QuantizedGraphRepository::deserialize, QuantizedGraph.h:130-150)
+  q.has_grp = false;
+  {
+    Reader r;
+    if (r.open(qd + "/grp")) {
+      const uint64_t Mfile = r.get<uint64_t>(), n = r.get<uint64_t>();
+      if (Mfile != q.M) return "qg/grp subspace count differs from qg/prf";
+      const uint64_t me = (q.M + 1) / 2 * 2;
+      q.qoff.assign(n + 1, 0);
+      q.code_off.assign(n + 1, 0);
+      q.qids.clear();
+      q.qcodes.clear();
+      for (uint64_t v = 0; v < n && r.ok; v++) {
+        uint32_t cnt = r.get<uint32_t>();
+        for (uint32_t i = 0; i < cnt && r.ok; i++) q.qids.push_back(r.get<uint32_t>());
+        const uint64_t nb = cnt == 0 ? 0 : (cnt - 1) / 16 + 1;
+        const size_t bytes = (size_t)(nb * 8 * me);
+        const size_t at = q.qcodes.size();
+        q.qcodes.resize(at + bytes);
+        r.bytes(q.qcodes.data() + at, bytes);
+        q.qoff[v + 1] = q.qids.size();
+        q.code_off[v + 1] = q.qcodes.size();
+      }
+      if (!r.ok) return "truncated qg/grp";
+      q.has_grp = true;
+    }
+  }
+  return "";
+}
+
+}  // namespace ngt_amd

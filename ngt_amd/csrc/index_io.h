@@ -75,10 +75,24 @@ struct HostIndex {
   void init_layout();
 };
 
+// NGTQG quantizer of <index>/qg (NGTQ::Index, lib/NGT/NGTQ/Quantizer.h) and,
+// when saved, its quantized graph qg/grp (QuantizedGraph.h:117-150).
+struct HostQuantizer {
+  uint32_t dim = 0, M = 0, dsub = 0;
+  std::vector<float> global;          // [dim] global centroid 1
+  std::vector<float> local;           // [M][16][dsub] local centroids 1..16
+  std::vector<uint8_t> codes;         // [nrows][M] localID - 1 (qg/ivt)
+  bool has_grp = false;
+  std::vector<uint64_t> qoff, code_off;
+  std::vector<uint32_t> qids;
+  std::vector<uint8_t> qcodes;
+};
+
 // All return an empty string on success, else an error message.
 std::string read_prf(const std::string& path, HostProperty& p);
 std::string write_prf(const std::string& path, HostProperty& p);
 std::string load_index(const std::string& dir, HostIndex& ix);
 std::string save_index(const std::string& dir, HostIndex& ix);
+std::string load_qg(const std::string& dir, uint64_t nrows, HostQuantizer& q);
 
 }  // namespace ngt_amd

@@ -26,11 +26,11 @@ def header_functions(path):
     return sorted({n for n in names if n.startswith(("ngt_", "ngtqg_")) and n not in skip})
 
 
-@pytest.mark.parametrize("hdr", ["include/ngt_amd.h", "include/NGT/Capi.h"])
+@pytest.mark.parametrize("hdr", ["include/ngt_amd.h", "include/NGT/Capi.h", "include/NGT/NGTQ/Capi.h"])
 def test_library_exports_every_declared_symbol(hdr):
     L = ngt_amd.lib()
     names = header_functions(os.path.join(ROOT, hdr))
-    assert len(names) > 10
+    assert len(names) >= 7
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
 
@@ -108,3 +108,24 @@ def test_edge_size_resolution_matches_getEdgeSize():
     # NeighborhoodGraph::getEdgeSize (Graph.h:675-692); host logic, no device needed
     if ngt_amd.device_count() == 0:
         pytest.skip("ngt_amd_index_create needs a device")
+
+
+def test_ngtqg_host_conventions():
+    """ngtqg_* defaults and error convention (NGTQ/Capi.cpp:40-131) without a device."""
+    import ctypes
+    from ngt_amd._sigs import NGTQGQuantizationParameters, NGTQGQuery
+    L = ngt_amd.lib()
+    q = NGTQGQuery()
+    L.ngtqg_initialize_query(ctypes.byref(q))
+    assert (q.size, round(q.epsilon, 6), q.result_expansion) == (20, 0.03, 3.0)
+    assert q.radius == np.float32(3.402823466e38)
+    p = NGTQGQuantizationParameters()
+    L.ngtqg_initialize_quantization_parameters(ctypes.byref(p))
+    assert (p.dimension_of_subvector, p.max_number_of_edges) == (0.0, 128)
+    err = L.ngt_create_error_object()
+    assert not L.ngtqg_open_index(b"/nonexistent/index", err)
+    assert L.ngt_get_error_string(err).decode().startswith("Capi : ngtqg_open_index() : Error:")
+    assert not L.ngtqg_search_index(None, q, None, err)
+    assert "ngtqg_search_index() : parametor error" in L.ngt_get_error_string(err).decode()
+    L.ngtqg_close_index(None)
+    L.ngt_destroy_error_object(err)

@@ -175,3 +175,35 @@ def test_qg_edge_cases():
             assert list(gi[qi, :gn[qi]]) == list(oid), (k, eps, exp, rad, qi)
             assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32))
     ix.close()
+
+
+@pytest.mark.parametrize("with_grp", [False, True])
+def test_ngtqg_capi_matches_reference(tmp_path, with_grp):
+    """The drop-in ngtqg_open_index / ngtqg_search_index path (NGTQ/Capi.cpp:52-115)
+    on the C1 ONNG + its reference-quantized qg/ directory, with the quantized
+    graph constructed on open (no qg/grp) or read from a saved qg/grp."""
+    import shutil
+    from ngt_amd.qg import QuantizedIndex
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("c1_qg")
+    d = tmp_path / "idx"
+    d.mkdir()
+    for f in ["prf", "obj", "grp", "tre"]:
+        os.symlink(os.path.join(GOLD, "c1_onng", f), str(d / f))
+    shutil.copytree(os.path.join(GOLD, "c1_qg", "qg"), str(d / "qg"))
+    if with_grp:
+        with open(str(d / "qg" / "grp"), "wb") as f:
+            f.write(F.serialize_qg_grp(qg))
+    ix = QuantizedIndex(str(d))
+    qs = z["queries"].astype(np.float32)
+    for key, k, eps, exp in _params(meta):
+        for qi in range(0, len(qs), 7):
+            r = ix.search(qs[qi], size=k, epsilon=eps, result_expansion=exp)
+            n = int(z["n_" + key][qi])
+            assert [i for i, _ in r] == [int(x) - 1 for x in z["ids_" + key][qi][:n]], (key, qi)
+            assert np.array_equal(np.array([dd for _, dd in r], np.float32).view(np.uint32),
+                                  z["dist_" + key][qi][:n].view(np.uint32)), (key, qi)
+        bi, bd, bn = ix.batch_search(qs, size=k, epsilon=eps, result_expansion=exp)
+        for qi in range(len(qs)):
+            n = int(z["n_" + key][qi])
+            assert int(bn[qi]) == n and list(bi[qi, :n]) == list(z["ids_" + key][qi][:n]), (key, qi)
+    ix.close()
