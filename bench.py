@@ -2,22 +2,31 @@
 """bench.py -- NGT distance hot path on MI355X.
 
 Metric (BASELINE.json): QPS at recall@10 = 0.95 on 1M x 128-d float L2
-(config 2: 1M synthetic U[0,1) vectors, ONNG-style graph, 1 x MI355X), plus the
+(config C2: 1M synthetic U[0,1) vectors, ONNG-style graph, 1 x MI355X), plus the
 search kernel's achieved HBM GB/s against the 8 TB/s peak.
 
 A *step* = one batched best-first search (NeighborhoodGraph::searchReadOnlyGraph
 semantics, lib/NGT/Graph.cpp:398-495) of the 10,000-query batch over the index,
 with queries, seeds, objects and graph already resident in HBM.
 
+Modes (`--mode`; the default is the headline):
+  exact  C2 (or `--config c3`: 1M x 960 cosine).  With N ranks every rank
+         searches its own 10,000-query batch on its own replica ("replicas",
+         weak scaling, no collective in the data path).
+  qg     the NGTQG quantized graph (QuantizedGraph.h:192-320) on the same
+         graph: 4-bit codes, dsub = 1 (M = 128 subspaces x 16 centroids),
+         exact rerank of k * result_expansion (C5's per-GPU search shape).
+  shard  C4's form: the object repository sharded one shard per rank (--n
+         objects per rank, global ids offset by rank), every rank searches
+         every query on its shard, RCCL all-gather of the per-shard top-k and
+         a device merge (ngt_amd/shard.py); QPS of the whole sharded index.
+
 Untimed setup: deterministic splitmix64 data (base seed 0x4E4754, queries
 base+1), graph construction (exact kNN by torch GEMM + top-k, then the
 ONNG-style out/in edge selection), exact ground truth with the HIP linear
 search, and an epsilon sweep to the smallest epsilon with recall@10 >= 0.95.
-
-Multi-GPU (torchrun): every rank searches its own 10,000-query batch on its own
-replica of the index ("replicas", weak scaling); no collective sits in the
-data path.  Timing: barrier + synchronize on both sides of exactly K steps, max
-over ranks, rank 0 prints one JSON line.
+Timing: barrier + synchronize on both sides of exactly K steps, max over
+ranks, rank 0 prints one JSON line.
 """
 import argparse
 import ctypes
@@ -33,6 +42,7 @@ sys.path.insert(0, ROOT)
 
 BASE_SEED = 0x4E4754
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+HEADLINE = "QPS at recall@10=0.95, 1M x 128-d float L2; achieved HBM GB/s vs peak"
 
 
 def log(*a):
@@ -41,16 +51,19 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------
-# data: splitmix64 -> float((x >> 40) * 2^-24), identical in every container
+# data: splitmix64 -> float((x >> 40) * 2^-24), identical in every container.
+# Element e of the stream (row-major over the whole data set) depends only on
+# e, so a shard generates its own rows without the others.
 # ---------------------------------------------------------------------------
-def splitmix_uniform(n, d, seed, chunk=1 << 22):
+def splitmix_uniform(n, d, seed, row0=0, chunk=1 << 22):
     out = np.empty(n * d, np.float32)
     gamma = np.uint64(0x9E3779B97F4A7C15)
     m1, m2 = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
+    e0 = row0 * d
     with np.errstate(over="ignore"):
         for s in range(0, n * d, chunk):
             e = min(n * d, s + chunk)
-            z = np.uint64(seed) + (np.arange(s + 1, e + 1, dtype=np.uint64) * gamma)
+            z = np.uint64(seed) + (np.arange(e0 + s + 1, e0 + e + 1, dtype=np.uint64) * gamma)
             z = (z ^ (z >> np.uint64(30))) * m1
             z = (z ^ (z >> np.uint64(27))) * m2
             z = z ^ (z >> np.uint64(31))
@@ -61,23 +74,29 @@ def splitmix_uniform(n, d, seed, chunk=1 << 22):
 # ---------------------------------------------------------------------------
 # graph construction (setup only; SURVEY.md 8(f) row 1 is the native builder)
 # ---------------------------------------------------------------------------
-def build_graph(torch, X, knn_k, out_deg, in_deg, max_deg, dev, chunk=4096):
+def build_graph(torch, X, knn_k, out_deg, in_deg, max_deg, dev, cosine=False, chunk=4096):
     """X: [N, D] float32 on device (objects 1..N).  Returns CSR (offsets[N+2],
     edges) over ids 1..N with each list sorted by (distance, id)."""
     N = X.shape[0]
-    norms = (X * X).sum(1)
+    if cosine:
+        Xn = X / X.norm(dim=1, keepdim=True).clamp_min(1e-30)
+    else:
+        norms = (X * X).sum(1)
     knn_i = torch.empty((N, knn_k), dtype=torch.int32, device=dev)
     knn_d = torch.empty((N, knn_k), dtype=torch.float32, device=dev)
     t0 = time.time()
     for s in range(0, N, chunk):
         e = min(N, s + chunk)
-        d = torch.addmm(norms[None, :], X[s:e], X.t(), beta=1.0, alpha=-2.0)
-        d += norms[s:e, None]
+        if cosine:
+            d = 1.0 - Xn[s:e] @ Xn.t()
+        else:
+            d = torch.addmm(norms[None, :], X[s:e], X.t(), beta=1.0, alpha=-2.0)
+            d += norms[s:e, None]
         r = torch.arange(e - s, device=dev)
         d[r, r + s] = float("inf")
         v, i = torch.topk(d, knn_k, dim=1, largest=False, sorted=True)
         knn_i[s:e] = i.to(torch.int32)
-        knn_d[s:e] = v.clamp_min(0).sqrt()
+        knn_d[s:e] = v.clamp_min(0) if cosine else v.clamp_min(0).sqrt()
         del d, v, i
     torch.cuda.synchronize()
     log("kNN(%d) over %d objects in %.1f s" % (knn_k, N, time.time() - t0))
@@ -95,7 +114,6 @@ def build_graph(torch, X, knn_k, out_deg, in_deg, max_deg, dev, chunk=4096):
     d_all = torch.cat([fd, rd])
     w_all = torch.cat([fw, rw])
     del fs, fd, fw, rs, rd, rw
-    # dedup (src, dst)
     key = s_all * N + d_all
     key, order = torch.sort(key)
     keep = torch.ones_like(key, dtype=torch.bool)
@@ -109,7 +127,6 @@ def build_graph(torch, X, knn_k, out_deg, in_deg, max_deg, dev, chunk=4096):
     s_all, d_all, w_all = s_all[o], d_all[o], w_all[o]
     o = torch.argsort(s_all, stable=True)
     s_all, d_all = s_all[o], d_all[o]
-    # cap the degree
     counts = torch.bincount(s_all, minlength=N)
     starts = torch.cumsum(counts, 0) - counts
     rank = torch.arange(s_all.numel(), device=dev) - starts[s_all]
@@ -123,6 +140,31 @@ def build_graph(torch, X, knn_k, out_deg, in_deg, max_deg, dev, chunk=4096):
     log("graph: %d edges, mean degree %.1f, max %d (%.1f s)" % (
         edges.numel(), edges.numel() / N, int(counts.max()), time.time() - t0))
     return offsets, edges
+
+
+def quantize_dsub1(torch, X, iters=12, sample=100_000):
+    """NGTQG codebooks for dsub = 1 (QuantizedGraph.h:374-385: D <= 400): 16
+    centroids per dimension by Lloyd iterations on a sample (setup only), the
+    global centroid is the zero vector (:397-399).  Returns local [M,16,1] and
+    codes [N, M] (localID - 1) of the objects."""
+    N, D = X.shape
+    g = torch.Generator(device=X.device).manual_seed(7)
+    idx = torch.randint(0, N, (min(sample, N),), device=X.device, generator=g)
+    S = X[idx]                                                     # [s, D]
+    qs = (torch.arange(16, device=X.device, dtype=torch.float32) + 0.5) / 16
+    C = torch.quantile(S, qs, dim=0).t().contiguous()              # [D, 16]
+    for _ in range(iters):
+        a = (S.t()[:, :, None] - C[:, None, :]).abs().argmin(2)    # [D, s]
+        for c in range(16):
+            m = (a == c).float()
+            cnt = m.sum(1)
+            C[:, c] = torch.where(cnt > 0, (m * S.t()).sum(1) / cnt.clamp_min(1), C[:, c])
+        C, _ = C.sort(1)
+    codes = torch.empty((N, D), dtype=torch.uint8, device=X.device)
+    for s in range(0, N, 65536):
+        e = min(N, s + 65536)
+        codes[s:e] = (X[s:e, :, None] - C[None]).abs().argmin(2).to(torch.uint8)
+    return C[:, :, None].contiguous(), codes
 
 
 def random_seeds(nrows, nq, seed_size):
@@ -150,13 +192,34 @@ def recall_at(ids, gt, k):
     return hit / float(gt.shape[0] * k)
 
 
+def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.002):
+    """Smallest epsilon whose mean recall@k reaches the target (ngt eval
+    semantics, Optimizer.h:400): given candidates, or by doubling + bisection."""
+    if eps_list:
+        for eps in eps_list:
+            if measure(eps) >= target:
+                return eps
+        return eps_list[-1]
+    while measure(hi) < target and hi < 4.0:
+        lo, hi = hi, hi * 2
+    while hi - lo > tol:
+        mid = 0.5 * (lo + hi)
+        if measure(mid) >= target:
+            hi = mid
+        else:
+            lo = mid
+    return hi
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000)
-    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--mode", choices=["exact", "qg", "shard"], default="exact")
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--n", type=int, default=0, help="objects (per shard in --mode shard)")
+    ap.add_argument("--dim", type=int, default=0)
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--target", type=float, default=0.95)
@@ -166,11 +229,23 @@ def main():
     ap.add_argument("--max-deg", type=int, default=160)
     ap.add_argument("--seed-size", type=int, default=10)
     ap.add_argument("--eps", type=str, default="")
+    ap.add_argument("--expansion", type=float, default=3.0, help="NGTQG result_expansion")
+    ap.add_argument("--qg-edges", type=int, default=128, help="NGTQG max edges per node")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--visited", type=int, default=-1,
-                    help="visited set: -1 HBM bitmap (this workload visits ~1e5 ids/query), 0 LDS hash")
+                    help="visited set: -1 HBM epochs (C2 visits ~1e5 ids/query), 0 LDS hash")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: everything else written to fd 1
+    # (RCCL's init banner, library chatter) goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    c3 = args.config == "c3"
+    if not args.n:
+        args.n = 1_250_000 if args.mode == "shard" else 1_000_000
+    if not args.dim:
+        args.dim = 960 if c3 else 128
+    metric = "cosine" if c3 else "l2"
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
@@ -179,39 +254,56 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if world > 1 or args.mode == "shard":
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from ngt_amd.device import COUNTERS, SEED_GIVEN, DeviceIndex
 
     N, D, NQ, K = args.n, args.dim, args.nq, args.k
     dp = ((D - 1) // 16 + 1) * 16
+    shard = args.mode == "shard"
     t0 = time.time()
-    base = splitmix_uniform(N, D, BASE_SEED)
-    qry = splitmix_uniform(NQ, D, BASE_SEED + 1 + rank * 0x1000)
+    if shard:
+        from ngt_amd.shard import ShardedIndex
+        offset = rank * N
+        base = splitmix_uniform(N, D, BASE_SEED, row0=offset)
+        qry = splitmix_uniform(NQ, D, BASE_SEED + 1)
+    else:
+        offset = 0
+        base = splitmix_uniform(N, D, BASE_SEED)
+        qry = splitmix_uniform(NQ, D, BASE_SEED + 1 + rank * 0x1000)
     log("data generated in %.1f s" % (time.time() - t0))
 
     # HBM layout: padded row-major slab, row 0 = dummy (ObjectRepository.h:37-40)
     rows = torch.zeros((N + 1, dp), dtype=torch.float32, device=dev)
     rows[1:, :D] = torch.from_numpy(base).to(dev)
-    qdev = torch.zeros((NQ, dp), dtype=torch.float32, device=dev)
-    qdev[:, :D] = torch.from_numpy(qry).to(dev)
-    offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev)
+    qraw = torch.from_numpy(qry).to(dev)
+    offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev,
+                                 cosine=c3)
 
-    ix = DeviceIndex("l2", "float", D, device=local)
+    ix = DeviceIndex(metric, "float", D, device=local)
     ix.set_objects_device(rows.data_ptr(), N + 1)
     ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
     ix.set_search_property(0, 30, 20, args.seed_size, 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    # queries prepared on the device like Index::allocateObject (pad; normalize
+    # for the normalized metrics)
+    qdev = torch.zeros((NQ, dp), dtype=torch.float32, device=dev)
+    ix.prepare_queries_device(qraw.data_ptr(), NQ, qdev.data_ptr(), stream=stream)
+    sx = ShardedIndex(torch, dist, ix, offset, dev) if shard else None
 
     # exact ground truth with the HIP linear search (linearSearch semantics)
     t0 = time.time()
     gt_i = torch.zeros((NQ, K), dtype=torch.int32, device=dev)
     gt_d = torch.zeros((NQ, K), dtype=torch.float32, device=dev)
     gt_n = torch.zeros((NQ,), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
     ix.linear_search_device(qdev.data_ptr(), dp * 4, NQ, K, gt_i.data_ptr(), gt_d.data_ptr(), gt_n.data_ptr(),
                             stream=stream)
+    if shard:
+        gt_i, gt_d, gt_n = sx.merge_local(gt_i, gt_d, gt_n, K, stream)
     torch.cuda.synchronize()
     gt = gt_i.cpu().numpy()
     log("ground truth in %.1f s" % (time.time() - t0))
@@ -223,52 +315,50 @@ def main():
     out_d = torch.zeros((NQ, K), dtype=torch.float32, device=dev)
     out_n = torch.zeros((NQ,), dtype=torch.int32, device=dev)
     cnt = torch.zeros((NQ, COUNTERS), dtype=torch.int64, device=dev)
+    result = {"ids": out_i}
+
+    if args.mode == "qg":
+        t0 = time.time()
+        local_cb, codes = quantize_dsub1(torch, rows[1:, :D])
+        h_codes = np.zeros((N + 1, D), np.uint8)
+        h_codes[1:] = codes.cpu().numpy()
+        ix.qg_set_quantizer(np.zeros(D, np.float32), local_cb.cpu().numpy())
+        ix.qg_build_graph(h_codes, args.qg_edges)
+        del codes
+        log("quantizer + quantized graph in %.1f s (degree <= %d)" % (time.time() - t0, ix.qg_max_degree()))
 
     def run(eps):
+        if args.mode == "qg":
+            ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, out_i.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                                cnt.data_ptr(), k=K, epsilon=eps, result_expansion=args.expansion,
+                                seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
+                                stream=stream, visited_hash_log2=args.visited)
+            return
         ix.search_device(qdev.data_ptr(), dp * 4, NQ, out_i.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
                          cnt.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
                          d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=stream,
                          visited_hash_log2=args.visited)
+        if shard:
+            result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
 
-    # epsilon search (ngt eval semantics: mean recall@k over the queries):
-    # the smallest epsilon whose recall@k reaches the target, by bisection
     sweep = []
 
     def measure(eps):
         run(eps)
         torch.cuda.synchronize()
-        r = recall_at(out_i.cpu().numpy(), gt, K)
+        r = recall_at(result["ids"].cpu().numpy(), gt, K)
         sweep.append((round(eps, 5), r, ix.last_search_kernel_ms()))
         log("eps %.4f recall@%d %.4f kernel %.2f ms" % (eps, K, r, sweep[-1][2]))
         return r
 
-    if args.eps:
-        cands = [float(x) for x in args.eps.split(",")]
-        chosen = cands[-1]
-        for eps in cands:
-            if measure(eps) >= args.target:
-                chosen = eps
-                break
-    else:
-        lo, hi = 0.0, 0.05
-        while measure(hi) < args.target and hi < 2.0:
-            lo, hi = hi, hi * 2
-        while hi - lo > 0.002:
-            mid = 0.5 * (lo + hi)
-            if measure(mid) >= args.target:
-                hi = mid
-            else:
-                lo = mid
-        chosen = hi
+    chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None)
     rec = measure(chosen)
-    if dist is not None:
-        # all ranks use the largest epsilon any rank needed
+    if dist is not None and not shard:
+        # replicas: all ranks use the largest epsilon any rank needed
         t = torch.tensor([chosen], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         chosen = float(t.item())
-        run(chosen)
-        torch.cuda.synchronize()
-        rec = recall_at(out_i.cpu().numpy(), gt, K)
+        rec = measure(chosen)
 
     for _ in range(args.warmup):
         run(chosen)
@@ -295,28 +385,50 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    qps = NQ * world * args.steps / elapsed
+    # replicas: every rank searched its own batch; shard: every rank searched
+    # the same batch on its part of one index
+    qps = NQ * (1 if shard else world) * args.steps / elapsed
 
-    # roofline of the search kernel: algorithmic bytes per launch
-    # B(q) = U(q)*Dp*4 + E(q)*4 + Dp*4 + k*8   
     c = cnt.cpu().numpy().astype(np.float64)
-    U, E = c[:, 0].sum(), c[:, 4].sum()
-    if "stamps" in os.environ.get("NGT_AMD_LIB", ""):
+    kernel_ms = float(np.mean(kms)) if kms else float("nan")
+    graph = "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg)
+    if args.mode == "qg":
+        # B(q) = sum_exp ceil(deg/16)*16*(M/2) + deg*4 + (seeds + k*expansion)*Dp*4  
+        me = (D + 1) // 2 * 2
+        alg_bytes = c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4 + NQ * (dp * 4 + K * 8)
+        kname = "ngt_qg_search_kernel"
+    else:
+        # B(q) = U(q)*Dp*4 + E(q)*4 + Dp*4 + k*8   
+        alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + NQ * (dp * 4 + K * 8)
+        kname = "ngt_graph_search_kernel"
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = measured_traffic(args.mode, args.config, graph, chosen)
+    if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
         tot = c[:, [5, 6, 7, 3]].mean(0)
         log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
             tot[0], tot[1], tot[2], tot[3], tot.sum()))
-    alg_bytes = U * dp * 4 + E * 4 + NQ * (dp * 4 + K * 8)
-    kernel_ms = float(np.mean(kms)) if kms else float("nan")
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = measured_traffic("kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg), chosen)
 
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
-        cpu = cpu_baseline(rows, offsets, edges, qry, seeds, chosen, K, dp, args.cpu_seconds)
+        cpu = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric)
 
     if rank == 0:
+        if args.mode == "exact" and not c3:
+            metric_name = HEADLINE
+            workload = "C2: %d x %d float L2 graph search, %d queries/step/GPU, k=%d" % (N, D, NQ, K)
+        elif args.mode == "exact":
+            metric_name = "QPS at recall@10=0.95, 1M x 960-d float cosine; achieved HBM GB/s vs peak"
+            workload = "C3: %d x %d float cosine graph search, %d queries/step/GPU, k=%d" % (N, D, NQ, K)
+        elif args.mode == "qg":
+            metric_name = "QPS at recall@10=0.95, %d x %d-d NGTQG quantized graph (L2); achieved HBM GB/s" % (N, D)
+            workload = "C5 shape per GPU: %d x %d NGTQG (dsub=1, M=%d, 16 centroids), result_expansion %g, " \
+                       "%d queries/step/GPU, k=%d" % (N, D, D, args.expansion, NQ, K)
+        else:
+            metric_name = "QPS at recall@10=0.95, %d x %d-d float L2 sharded over %d GPUs" % (N * world, D, world)
+            workload = "C4 form: %d objects per GPU shard, %d shards, %d queries/step over all shards, k=%d, " \
+                       "RCCL all-gather of per-shard top-k + device merge" % (N, world, NQ, K)
         line = {
-            "metric": "QPS at recall@10=0.95, 1M x 128-d float L2; achieved HBM GB/s vs peak",
+            "metric": metric_name,
             "value": qps,
             "unit": "queries/s",
             "n_gpus": world,
@@ -326,68 +438,105 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.mode != "qg" else "u4-adc/u8-lut/f32-rerank",
             "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
-            "config": {"workload": "C2: %d x %d float L2 graph search, %d queries/step/GPU, k=%d" % (N, D, NQ, K),
-                       "recall_at_10": rec, "epsilon": chosen, "edge_size": "all",
-                       "graph": "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg),
+            "config": {"workload": workload,
+                       "recall_at_10": rec, "epsilon": chosen, "edge_size": "all", "graph": graph,
                        "seeds": "getRandomSeeds (%d)" % args.seed_size,
-                       "distance_computations_per_query": U / NQ,
+                       "distance_computations_per_query": float(c[:, 0].mean()),
                        "expansions_per_query": float(c[:, 2].mean()),
-                       "edges_read_per_query": E / NQ,
-                       "max_unchecked_per_query": float(c[:, 5].max()),
-                       "visited_set": "hbm-bitmap" if args.visited < 0 else "lds-hash",
-                       "parallelism": "replicas x%d" % world},
+                       "visited_set": "hbm-epochs" if args.visited < 0 else "lds-hash",
+                       "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "sweep": sweep,
         }
-        print(json.dumps(line), flush=True)
+        if args.mode == "qg":
+            line["config"]["result_expansion"] = args.expansion
+            line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
+            line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
+        else:
+            line["config"]["edges_read_per_query"] = float(c[:, 4].mean())
+        print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def measured_traffic(graph, eps):
+def measured_traffic(mode, config, graph, eps):
     """HBM bytes per launch of the search kernel from the committed PMC passes
     (profiles/traffic.json, written from rocprofv3 FETCH_SIZE/WRITE_SIZE) for this
-    exact graph and epsilon; NGT_BENCH_TRAFFIC_BYTES overrides; else None."""
+    exact workload and epsilon; NGT_BENCH_TRAFFIC_BYTES overrides; else None."""
     tf = os.environ.get("NGT_BENCH_TRAFFIC_BYTES")
     if tf:
         return float(tf)
     try:
-        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")) as f:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
         return None
     for e in entries:
-        if e["graph"] == graph and abs(e["epsilon"] - eps) < 1e-7:
+        if (e.get("mode", "exact") == mode and e.get("config", "c2") == config and e["graph"] == graph
+                and abs(e["epsilon"] - eps) < 1e-7):
             return float(e["traffic_bytes"])
     return None
 
 
-def cpu_baseline(rows, offsets, edges, qry, seeds, eps, K, dp, budget_s):
+def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric):
     """The oracle restatement (scalar, 1 thread) on a bounded sample of the
-    same workload: same graph, seeds and epsilon, queries until the budget."""
+    same workload: same graph, seeds and epsilon (and quantized graph for qg),
+    queries until the budget."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     t0 = time.time()
     h_rows = rows.cpu().numpy()
     h_off = offsets.cpu().numpy().astype(np.uint64)
     h_edges = edges.cpu().numpy().astype(np.uint32)
+    h_q = qdev.cpu().numpy()
+    qg = None
+    if args.mode == "qg":
+        ids, codes = ix.qg_get_graph()
+        deg = (ids != 0).sum(1).astype(np.uint64)
+        qoff = np.zeros(len(deg) + 1, np.uint64)
+        qoff[1:] = np.cumsum(deg)
+        qg = {"M": args.dim, "dim": args.dim, "dsub": 1, "qoff": qoff, "qids": ids[ids != 0].astype(np.uint32),
+              "code_off": (np.arange(len(deg) + 1, dtype=np.uint64) * np.uint64(codes.shape[1])),
+              "codes": codes.reshape(-1), "global": np.zeros(args.dim, np.float32),
+              "local": None}
+        lut, sc, to = ix.qg_lut(h_q[:, :args.dim])
     log("cpu baseline: host copy %.1f s" % (time.time() - t0))
     done = 0
     t0 = time.perf_counter()
-    while done < qry.shape[0] and time.perf_counter() - t0 < budget_s:
-        q = np.zeros(dp, np.float32)
-        q[:qry.shape[1]] = qry[done]
-        O.search("l2", h_rows, h_off, h_edges, q, seeds[done], K, np.float32(eps), edge_size=0)
+    while done < h_q.shape[0] and time.perf_counter() - t0 < args.cpu_seconds:
+        if qg is not None:
+            oracle_qg_search(O, qg, h_rows, h_q[done], seeds[done], args.k, eps, args.expansion, lut[done],
+                             sc[done], to[done])
+        else:
+            O.search(metric, h_rows, h_off, h_edges, h_q[done], seeds[done], args.k, np.float32(eps), edge_size=0)
         done += 1
     el = time.perf_counter() - t0
+    what = ("NGTQG::Index::searchQuantizedGraph restatement (LUT as input)" if qg is not None
+            else "searchReadOnlyGraph restatement")
     return {"value": done / el, "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": "%d of the 10000 queries (same graph, seeds, epsilon), oracle/ngt_oracle.c "
-                      "searchReadOnlyGraph restatement, 1 thread, %.1f s" % (done, el)}
+            "sample": "%d of the %d queries (same graph, seeds, epsilon), oracle/ngt_oracle.c %s, 1 thread, %.1f s"
+                      % (done, h_q.shape[0], what, el)}
+
+
+def oracle_qg_search(O, qg, rows, q, seeds, k, eps, expansion, lut, sc, to):
+    L = O.lib()
+    O._qg_sigs(L)
+    p = O._p
+    ids = np.zeros(max(k, int(k * expansion) + 1), np.uint32)
+    ds = np.zeros_like(ids, dtype=np.float32)
+    cnt = np.zeros(4, np.uint64)
+    q = np.ascontiguousarray(q, np.float32)
+    s = np.ascontiguousarray(seeds, np.uint32)
+    L.ngto_qg_search(p(rows, ctypes.c_float), rows.shape[1], rows.shape[0], p(qg["qoff"], ctypes.c_uint64),
+                     p(qg["qids"], ctypes.c_uint32), p(qg["code_off"], ctypes.c_uint64),
+                     p(qg["codes"], ctypes.c_uint8), qg["M"], p(np.ascontiguousarray(lut), ctypes.c_uint8),
+                     float(sc), float(to), p(q, ctypes.c_float), p(s, ctypes.c_uint32), len(s), k, eps, expansion,
+                     3.402823466e38, p(ids, ctypes.c_uint32), p(ds, ctypes.c_float), p(cnt, ctypes.c_uint64))
 
 
 if __name__ == "__main__":

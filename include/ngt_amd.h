@@ -159,6 +159,18 @@ int ngt_amd_prepare_queries_device(ngt_amd_index *index, const float *d_in, uint
 /* Timing of the last search call's kernels (HIP events on the search stream), ms. */
 float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
 
+/* ---- repository sharding (one shard per GPU) ------------ *
+ * Merge of per-shard result lists gathered from every rank (RCCL all-gather
+ * over xGMI): the k best (distance, global id) per query, the ordering of
+ * NGT::ObjectDistance (lib/NGT/Common.h:1946-1959) -- the result a single
+ * index over the union would rank.  d_ids/d_dists: [nparts][nq][k] sorted
+ * shard-local results, d_n: [nparts][nq] valid entries; id_offsets (host):
+ * [nparts] added to shard-local ids.  Outputs [nq][k] and [nq]. */
+int ngt_amd_merge_results_device(int device, const uint32_t *d_ids, const float *d_dists,
+                                 const uint32_t *d_n, uint32_t nparts, uint32_t nq, uint32_t k,
+                                 const uint32_t *id_offsets, uint32_t *d_out_ids, float *d_out_dists,
+                                 uint32_t *d_out_n, void *stream);
+
 /* ---- NGTQG quantized graph (L2, float objects) -------------------------- *
  *   ngt_amd_qg_set_quantizer  <- the NGTQ::Quantizer NGTQG::Index opens from
  *                                <index>/qg (lib/NGT/NGTQ/QuantizedGraph.h:170-185):
@@ -195,6 +207,12 @@ int ngt_amd_qg_set_graph(ngt_amd_index *index, const uint64_t *qoff, const uint3
                          const uint64_t *code_off, const uint8_t *codes);
 /* Widest quantized neighbour list (row stride of ngt_amd_qg_adc's output). */
 uint32_t ngt_amd_qg_max_degree(const ngt_amd_index *index);
+/* Bytes of one node's code row (max degree / 16 blocks of 8 * Me bytes). */
+uint64_t ngt_amd_qg_code_stride(const ngt_amd_index *index);
+/* Copy the quantized graph back to the host (what QuantizedGraphRepository::
+ * serialize writes, QuantizedGraph.h:117-128): ids [nrows][max_degree]
+ * (0-terminated) and codes [nrows][code_stride] in the reference stream layout. */
+int ngt_amd_qg_get_graph(const ngt_amd_index *index, uint32_t *ids, uint8_t *codes);
 /* Per query: lut [nq][Me*16] bytes, scale [nq], total_offset [nq]. */
 int ngt_amd_qg_lut(ngt_amd_index *index, const float *queries, uint32_t nq, uint8_t *lut,
                    float *scale, float *total_offset);

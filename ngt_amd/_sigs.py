@@ -62,10 +62,14 @@ def declare(L):
         "ngt_amd_distances": (c_int, [vp, vp, c_uint32, vp, vp, c_uint64, vp]),
         "ngt_amd_prepare_queries_device": (c_int, [vp, vp, c_uint32, vp, vp]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
+        "ngt_amd_merge_results_device": (c_int, [c_int, vp, vp, vp, c_uint32, c_uint32, c_uint32, vp, vp, vp, vp,
+                                                 vp]),
         "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),
         "ngt_amd_qg_build_graph": (c_int, [vp, vp, c_uint32]),
         "ngt_amd_qg_set_graph": (c_int, [vp, vp, vp, vp, vp]),
         "ngt_amd_qg_max_degree": (c_uint32, [vp]),
+        "ngt_amd_qg_code_stride": (c_uint64, [vp]),
+        "ngt_amd_qg_get_graph": (c_int, [vp, vp, vp]),
         "ngt_amd_qg_lut": (c_int, [vp, vp, c_uint32, vp, vp, vp]),
         "ngt_amd_qg_adc": (c_int, [vp, vp, vp, vp, c_uint32, vp, vp, c_uint64, vp, vp]),
         "ngt_amd_qg_search": (c_int, [vp, POINTER(QgSearchParams), vp, c_uint32, vp, vp, vp, vp, vp, vp]),

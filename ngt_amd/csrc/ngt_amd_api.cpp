@@ -570,3 +570,34 @@ extern "C" int ngt_amd_distances(ngt_amd_index* ix, const void* queries, uint32_
   HIP_OK(hipStreamSynchronize(s));
   return 0;
 }
+
+extern "C" int ngt_amd_merge_results_device(int device, const uint32_t* d_ids, const float* d_dists,
+                                            const uint32_t* d_n, uint32_t nparts, uint32_t nq, uint32_t k,
+                                            const uint32_t* id_offsets, uint32_t* d_out_ids, float* d_out_dists,
+                                            uint32_t* d_out_n, void* stream) {
+  if (!d_ids || !d_dists || !d_n || !id_offsets || !d_out_ids || !d_out_dists || !d_out_n || nparts == 0 || k == 0)
+    return fail("ngt_amd_merge_results_device: bad arguments");
+  if ((uint64_t)nparts * k * sizeof(uint64_t) > 64 * 1024)
+    return fail("ngt_amd_merge_results_device: %u parts x k=%u exceed one workgroup's LDS", nparts, k);
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = (hipStream_t)stream;
+  DevBuf<uint32_t> off;
+  HIP_OK(off.alloc(nparts));
+  HIP_OK(hipMemcpyAsync(off.p, id_offsets, nparts * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  MergeArgs a{};
+  a.in_ids = d_ids;
+  a.in_dists = d_dists;
+  a.in_n = d_n;
+  a.id_offsets = off.p;
+  a.nparts = nparts;
+  a.nq = nq;
+  a.k = k;
+  a.out_ids = d_out_ids;
+  a.out_dists = d_out_dists;
+  a.out_n = d_out_n;
+  HIP_OK(launch_merge_results(a, s));
+  // `off` is freed on return: order the free after the kernel
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}

@@ -93,7 +93,19 @@ struct LinearArgs {
   uint32_t* out_n;
 };
 
+struct MergeArgs {
+  const uint32_t* in_ids;        // [nparts][nq][k] shard-local ids
+  const float* in_dists;         // [nparts][nq][k]
+  const uint32_t* in_n;          // [nparts][nq]
+  const uint32_t* id_offsets;    // [nparts] local -> global id offset
+  uint32_t nparts, nq, k;
+  uint32_t* out_ids;             // [nq][k] global ids
+  float* out_dists;
+  uint32_t* out_n;               // [nq]
+};
+
 hipError_t launch_distances(const DistanceArgs& a, int metric, int otype, hipStream_t s);
+hipError_t launch_merge_results(const MergeArgs& a, hipStream_t s);
 hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipStream_t s);
 size_t search_lds_bytes(const SearchArgs& a, int otype);
 hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,

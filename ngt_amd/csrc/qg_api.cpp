@@ -126,6 +126,20 @@ extern "C" uint32_t ngt_amd_qg_max_degree(const ngt_amd_index* ix) {
   return ix && ix->qg.has_graph ? ix->qg.id_stride : 0;
 }
 
+extern "C" uint64_t ngt_amd_qg_code_stride(const ngt_amd_index* ix) {
+  return ix && ix->qg.has_graph ? ix->qg.code_stride : 0;
+}
+
+extern "C" int ngt_amd_qg_get_graph(const ngt_amd_index* ix, uint32_t* ids, uint8_t* codes) {
+  if (!ix || !ids || !codes) return fail("ngt_amd_qg_get_graph: bad arguments");
+  if (!ix->qg.has_graph) return fail("ngt_amd_qg_get_graph: the index has no quantized graph");
+  HIP_OK(hipSetDevice(ix->device));
+  const QgState& q = ix->qg;
+  HIP_OK(hipMemcpy(ids, q.qids.p, (size_t)ix->nrows * q.id_stride * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(codes, q.qcodes.p, (size_t)ix->nrows * q.code_stride, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 // LUTs of nq prepared device queries into ix->qg.lut/scale/toff.
 static int run_lut(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq, hipStream_t s) {
   QgState& q = ix->qg;

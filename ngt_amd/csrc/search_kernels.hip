@@ -477,6 +477,43 @@ __global__ void __launch_bounds__(64) ngt_linear_merge_kernel(LinearArgs a, uint
 }
 
 // ---------------------------------------------------------------------------
+// Shard merge (repository sharded over GPUs): per query, the
+// k best (distance, global id) keys of nparts sorted per-shard result lists
+// gathered from every rank -- ObjectDistance ordering (Common.h:1946-1959),
+// so ties across shards resolve by id exactly as one index would.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) ngt_merge_results_kernel(MergeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
+  const int lane = lane_id();
+  const uint32_t total = a.nparts * a.k;
+  for (uint32_t qi = blockIdx.x; qi < a.nq; qi += gridDim.x) {
+    for (uint32_t i = lane; i < total; i += 64) {
+      const uint32_t s = i / a.k, j = i - s * a.k;
+      const uint64_t at = ((uint64_t)s * a.nq + qi) * a.k + j;
+      const uint32_t n = a.in_n[(uint64_t)s * a.nq + qi];
+      keys[i] = j < n ? make_key(a.in_dists[at], a.in_ids[at] + a.id_offsets[s]) : ~0ull;
+    }
+    __syncthreads();
+    uint32_t valid = 0;
+    for (uint32_t i = lane; i < total; i += 64) {
+      const uint64_t key = keys[i];
+      if (key == ~0ull) continue;
+      valid++;
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < total; j++) rank += keys[j] < key ? 1u : 0u;
+      if (rank < a.k) {
+        a.out_ids[(uint64_t)qi * a.k + rank] = key_id(key);
+        a.out_dists[(uint64_t)qi * a.k + rank] = key_dist(key);
+      }
+    }
+    valid = wave_sum_u32(valid);
+    if (lane == 0) a.out_n[qi] = valid < a.k ? valid : a.k;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launchers (dispatch on metric x object type).
 // ---------------------------------------------------------------------------
 #define NGT_DISPATCH(METRIC, OTYPE, LAUNCH)                                    \
@@ -580,6 +617,14 @@ hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint
   if (e != hipSuccess) return e;
   const size_t lds2 = ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   hipLaunchKernelGGL(ngt_linear_merge_kernel, dim3(a.nq), dim3(64), lds2, s, a, nslices);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_results(const MergeArgs& a, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = (size_t)a.nparts * a.k * sizeof(uint64_t);
+  const uint32_t blocks = a.nq < 16384 ? a.nq : 16384;
+  hipLaunchKernelGGL(ngt_merge_results_kernel, dim3(blocks), dim3(64), lds, s, a);
   return hipGetLastError();
 }
 

@@ -186,6 +186,15 @@ class DeviceIndex(object):
     def qg_max_degree(self):
         return int(self.L.ngt_amd_qg_max_degree(self.h))
 
+    def qg_get_graph(self):
+        """(ids [nrows, max_degree] 0-terminated, codes [nrows, code_stride])."""
+        md = self.qg_max_degree()
+        cs = int(self.L.ngt_amd_qg_code_stride(self.h))
+        ids = np.zeros((self.nrows, md), np.uint32)
+        codes = np.zeros((self.nrows, cs), np.uint8)
+        _chk(self.L.ngt_amd_qg_get_graph(self.h, ids.ctypes.data, codes.ctypes.data))
+        return ids, codes
+
     def qg_lut(self, queries):
         q = np.ascontiguousarray(queries, dtype=np.float32)
         nq = q.shape[0]

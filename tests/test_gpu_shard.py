@@ -1,0 +1,97 @@
+"""GPU side of the sharded path: the device merge kernel
+(ngt_amd_merge_results_device) against a numpy merge of the same lists, and
+the full ShardedIndex pipeline (local graph search -> RCCL all-gather ->
+device merge) on a one-rank nccl group, against the oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+
+def np_merge(ids, ds, n, offsets, k):
+    S, nq, _ = ids.shape
+    oi = np.zeros((nq, k), np.uint32)
+    od = np.zeros((nq, k), np.float32)
+    on = np.zeros(nq, np.uint32)
+    for q in range(nq):
+        c = sorted((float(ds[s, q, j]), int(ids[s, q, j]) + offsets[s]) for s in range(S) for j in range(n[s, q]))
+        for j, (d, i) in enumerate(c[:k]):
+            oi[q, j], od[q, j] = i, d
+        on[q] = min(k, len(c))
+    return oi, od, on
+
+
+@pytest.mark.parametrize("S,k", [(2, 10), (8, 10), (8, 100), (3, 1)])
+def test_merge_kernel_matches_numpy(S, k):
+    import torch
+    from ngt_amd.shard import merge_device
+    rng = np.random.default_rng(S * 100 + k)
+    nq = 300
+    ids = np.zeros((S, nq, k), np.uint32)
+    ds = np.zeros((S, nq, k), np.float32)
+    n = rng.integers(0, k + 1, size=(S, nq)).astype(np.uint32)
+    n[:, 0] = k
+    offsets = [s * 1000 for s in range(S)]
+    for s in range(S):
+        for q in range(nq):
+            d = np.sort(rng.integers(0, 50, k).astype(np.float32) / np.float32(7))  # many exact ties
+            ids[s, q] = rng.choice(np.arange(1, 1000), k, replace=False)
+            order = np.lexsort((ids[s, q], d))
+            ids[s, q], ds[s, q] = ids[s, q][order], d[order]
+    dev = torch.device("cuda:0")
+    gi, gd, gn = merge_device(torch, torch.from_numpy(ids.view(np.int32)).to(dev), torch.from_numpy(ds).to(dev),
+                              torch.from_numpy(n.view(np.int32)).to(dev), offsets, k)
+    torch.cuda.synchronize()
+    ei, ed, en = np_merge(ids, ds, n, offsets, k)
+    gi, gd, gn = gi.cpu().numpy().view(np.uint32), gd.cpu().numpy(), gn.cpu().numpy()
+    assert np.array_equal(gn, en)
+    for q in range(nq):
+        assert list(gi[q, :gn[q]]) == list(ei[q, :en[q]]), q
+        assert np.array_equal(gd[q, :gn[q]].view(np.uint32), ed[q, :en[q]].view(np.uint32))
+
+
+def test_sharded_index_one_rank_nccl():
+    import torch
+    import torch.distributed as dist
+    from ngt_amd.device import SEED_GIVEN, DeviceIndex
+    from ngt_amd.shard import ShardedIndex, shard_bounds
+    from test_gpu_parity import _random_graph
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda:0")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        n, dim, deg, nq = 4000, 32, 16, 64
+        rows, offs, edges = _random_graph(n, dim, deg, 9)
+        off, cnt = shard_bounds(n - 1, 1, 0)
+        ix = DeviceIndex("l2", "float", dim)
+        ix.set_objects(rows)
+        ix.set_graph(offs, edges)
+        rng = np.random.default_rng(4)
+        qs = rng.random((nq, dim), dtype=np.float32)
+        seeds = np.stack([rng.choice(np.arange(1, n), 8, replace=False) for _ in range(nq)]).astype(np.uint32)
+        d_q = torch.from_numpy(qs).to(dev)
+        d_s = torch.from_numpy(seeds.reshape(-1).view(np.int32)).to(dev)
+        d_o = torch.arange(0, nq + 1, dtype=torch.int64, device=dev) * 8
+        sx = ShardedIndex(torch, dist, ix, off, dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        gi, gd, gn = sx.search_device(d_q.data_ptr(), dim * 4, nq, 10, 0.2, seeds=d_s.data_ptr(),
+                                      seed_off=d_o.data_ptr(), stream=stream, edge_size=0, seed_mode=SEED_GIVEN)
+        torch.cuda.synchronize()
+        gi, gd, gn = gi.cpu().numpy().view(np.uint32), gd.cpu().numpy(), gn.cpu().numpy()
+        for i in range(nq):
+            oid, od, _ = O.search("l2", rows, offs, edges, qs[i], seeds[i], 10, np.float32(0.2))
+            assert list(gi[i, :gn[i]]) == list(oid + off), i
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32))
+        ix.close()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,123 @@
+"""The multi-GPU path (repository sharded one shard per rank)
+rehearsed on CPU with world_size 2 over gloo: shard bounds, the all-gather of
+per-shard result lists and the global-id merge must reproduce one index over
+the union.  Per-shard results come from the oracle's exact linear search
+(test infrastructure); the merge here is a numpy checker of the device
+merge's contract (tests/test_gpu_shard.py runs the device merge itself)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from ngt_amd.shard import ShardedIndex, shard_bounds
+
+N, DIM, NQ, K = 1500, 16, 12, 10
+
+
+def _data():
+    rng = np.random.default_rng(42)
+    rows = np.zeros((N + 1, DIM), np.float32)
+    rows[1:] = rng.random((N, DIM), dtype=np.float32)
+    # exact ties across shards: duplicate vectors in both halves
+    rows[N - 3] = rows[5]
+    rows[N - 2] = rows[6]
+    qs = rng.random((NQ, DIM), dtype=np.float32)
+    qs[0] = rows[5]
+    return rows, qs
+
+
+def numpy_merge(torch, g_ids, g_d, g_n, offsets, k, stream=None):
+    world, nq = g_n.shape[0], g_n.shape[1]
+    out_i = torch.zeros((nq, k), dtype=torch.int32)
+    out_d = torch.zeros((nq, k), dtype=torch.float32)
+    out_n = torch.zeros((nq,), dtype=torch.int32)
+    for q in range(nq):
+        cand = []
+        for s in range(world):
+            for j in range(int(g_n[s, q])):
+                cand.append((float(g_d[s, q, j]), int(g_ids[s, q, j]) + offsets[s]))
+        cand.sort()
+        for j, (d, i) in enumerate(cand[:k]):
+            out_i[q, j] = i
+            out_d[q, j] = d
+        out_n[q] = min(k, len(cand))
+    return out_i, out_d, out_n
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows, qs = _data()
+        off, cnt = shard_bounds(N, world, rank)
+        shard = np.zeros((cnt + 1, DIM), np.float32)
+        shard[1:] = rows[off + 1:off + 1 + cnt]
+        ids = np.zeros((NQ, K), np.int32)
+        ds = np.zeros((NQ, K), np.float32)
+        n = np.zeros(NQ, np.int32)
+        for i in range(NQ):
+            oi, od = O.linear_search("l2", shard, qs[i], K)[:2]
+            n[i] = len(oi)
+            ids[i, :n[i]] = oi
+            ds[i, :n[i]] = od
+        sx = ShardedIndex(torch, dist, None, off, torch.device("cpu"), merge=numpy_merge)
+        gi, gd, gn = sx.merge_local(torch.from_numpy(ids), torch.from_numpy(ds), torch.from_numpy(n), K)
+        q.put((rank, off, cnt, sx.offsets, gi.numpy(), gd.numpy(), gn.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_bounds_partition():
+    for n, w in [(10, 3), (1_000_000, 8), (7, 8), (12_500_000, 8)]:
+        spans = [shard_bounds(n, w, r) for r in range(w)]
+        assert sum(c for _, c in spans) == n
+        assert spans[0][0] == 0
+        for (o0, c0), (o1, _) in zip(spans, spans[1:]):
+            assert o1 == o0 + c0
+
+
+@pytest.mark.timeout(300)
+def test_sharded_search_equals_union_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    import queue
+    import time
+    outs = []
+    t0 = time.time()
+    while len(outs) < 2 and time.time() - t0 < 240:
+        try:
+            outs.append(q.get(timeout=2))
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert len(outs) == 2
+    outs.sort()
+    rows, qs = _data()
+    assert outs[0][3] == outs[1][3] == [outs[0][1], outs[1][1]]
+    for rank, off, cnt, offsets, gi, gd, gn in outs:
+        for i in range(NQ):
+            oi, od = O.linear_search("l2", rows, qs[i], K)[:2]
+            assert int(gn[i]) == len(oi)
+            assert list(gi[i, :gn[i]]) == list(oi), (rank, i)
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32))
