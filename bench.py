@@ -456,6 +456,7 @@ def main():
         if args.mode == "qg":
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
+            line["config"]["accepted_per_query"] = float(c[:, 1].mean())
             line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
         else:
             line["config"]["edges_read_per_query"] = float(c[:, 4].mean())
