@@ -407,6 +407,10 @@ def main():
         tot = c[:, [5, 6, 7, 3]].mean(0)
         log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
             tot[0], tot[1], tot[2], tot[3], tot.sum()))
+    if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "qg":
+        tot = c[:, [4, 5, 6, 7]].mean(0)
+        log("phase cycles/query: pop %.3g ids %.3g codes+adc %.3g accept %.3g (sum %.3g)" % (
+            tot[0], tot[1], tot[2], tot[3], tot.sum()))
 
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:

@@ -63,17 +63,54 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((uint64_t)hi << 32) | lo;
 }
+// Wave-wide reductions without LDS traffic: DPP inside each 16-lane row
+// (quad_perm lane^1 / lane^2, row_ror:4, row_ror:8 -- the last two turn quad
+// results into row results), then gfx950 v_permlane16_swap / v_permlane32_swap
+// across rows (odd rows trade with even rows, upper half with lower half), so
+// every lane ends with the wave's result.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+  return ((uint64_t)dpp_u32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp_u32<CTRL>((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return b < a ? b : a; }
+
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    uint64_t o = shfl_xor_u64(v, m);
-    v = o < v ? o : v;
+  v = min_u64(v, dpp_u64<0xb1>(v));   // quad_perm [1,0,3,2]
+  v = min_u64(v, dpp_u64<0x4e>(v));   // quad_perm [2,3,0,1]
+  v = min_u64(v, dpp_u64<0x124>(v));  // row_ror:4
+  v = min_u64(v, dpp_u64<0x128>(v));  // row_ror:8
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = min_u64(((uint64_t)h[0] << 32) | l[0], ((uint64_t)h[1] << 32) | l[1]);
+  }
+  lo = (uint32_t)v;
+  hi = (uint32_t)(v >> 32);
+  {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = min_u64(((uint64_t)h[0] << 32) | l[0], ((uint64_t)h[1] << 32) | l[1]);
   }
   return v;
 }
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
+  v += dpp_u32<0xb1>(v);
+  v += dpp_u32<0x4e>(v);
+  v += dpp_u32<0x124>(v);
+  v += dpp_u32<0x128>(v);
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = r[0] + r[1];
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = r[0] + r[1];
+  }
   return v;
 }
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }

@@ -126,14 +126,18 @@ __global__ void __launch_bounds__(256) ngt_qg_build_kernel(QgBuildArgs a) {
 // ---------------------------------------------------------------------------
 // ADC building blocks.
 // ---------------------------------------------------------------------------
-// Four table lookups: bytes of `idx` (each 0..15) index the 16-byte table
-// t0..t3 (little-endian dwords).
-__device__ __forceinline__ uint32_t lut16(uint32_t idx, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3) {
-  const uint32_t sel = idx & 0x07070707u;
+// Four table lookups into the 16-byte table t0..t3 (little-endian dwords):
+// byte b of the result = table[nibble of byte b of `w` at bit `sh`] for
+// sh = 0 (low nibbles) or 4 (high nibbles).  Two v_perm_b32 look the 3 low
+// index bits up in the lower and upper 8 table bytes; a third picks, per
+// byte, lower or upper by index bit 3 (selector b or 4 + b).
+template <int SH>
+__device__ __forceinline__ uint32_t lut16(uint32_t w, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3) {
+  const uint32_t sel = (w >> SH) & 0x07070707u;
   const uint32_t lo = __builtin_amdgcn_perm(t1, t0, sel);
   const uint32_t hi = __builtin_amdgcn_perm(t3, t2, sel);
-  const uint32_t m = ((idx >> 3) & 0x01010101u) * 0xffu;
-  return (hi & m) | (lo & ~m);
+  const uint32_t pick = ((w >> (SH + 1)) & 0x04040404u) | 0x03020100u;
+  return __builtin_amdgcn_perm(hi, lo, pick);
 }
 
 // Lane table of PPL subspace pairs: tab[s][0..3] even subspace 2p, [4..7] odd 2p+1.
@@ -169,14 +173,14 @@ __device__ __forceinline__ void block_partials(const LaneLut<PPL>& L, const uint
   for (int s = 0; s < PPL; s++) {
     const uint32_t* t = L.t[s];
     // even subspace: c.x = objects 0..7, c.y = 8..15 (low nibble = even object)
-    const uint32_t e0 = lut16(c[s].x & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);          // 0,2,4,6
-    const uint32_t e1 = lut16((c[s].x >> 4) & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);   // 1,3,5,7
-    const uint32_t e2 = lut16(c[s].y & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);          // 8,...,14
-    const uint32_t e3 = lut16((c[s].y >> 4) & 0x0f0f0f0fu, t[0], t[1], t[2], t[3]);   // 9,...,15
-    const uint32_t o0 = lut16(c[s].z & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
-    const uint32_t o1 = lut16((c[s].z >> 4) & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
-    const uint32_t o2 = lut16(c[s].w & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
-    const uint32_t o3 = lut16((c[s].w >> 4) & 0x0f0f0f0fu, t[4], t[5], t[6], t[7]);
+    const uint32_t e0 = lut16<0>(c[s].x, t[0], t[1], t[2], t[3]);  // objects 0,2,4,6
+    const uint32_t e1 = lut16<4>(c[s].x, t[0], t[1], t[2], t[3]);  // 1,3,5,7
+    const uint32_t e2 = lut16<0>(c[s].y, t[0], t[1], t[2], t[3]);  // 8,...,14
+    const uint32_t e3 = lut16<4>(c[s].y, t[0], t[1], t[2], t[3]);  // 9,...,15
+    const uint32_t o0 = lut16<0>(c[s].z, t[4], t[5], t[6], t[7]);
+    const uint32_t o1 = lut16<4>(c[s].z, t[4], t[5], t[6], t[7]);
+    const uint32_t o2 = lut16<0>(c[s].w, t[4], t[5], t[6], t[7]);
+    const uint32_t o3 = lut16<4>(c[s].w, t[4], t[5], t[6], t[7]);
     // byte b of (e_k, o_k) -> (E | O << 16): selector {b, zero, 4 + b, zero}
 #pragma unroll
     for (int b = 0; b < 4; b++) {
@@ -190,45 +194,49 @@ __device__ __forceinline__ void block_partials(const LaneLut<PPL>& L, const uint
 }
 
 // Reduce-scatter 16 per-lane values over the wave: on return every lane holds
-// the full sum of object qg_obj_of_lane(lane).
+// the full sum of object qg_obj_of_lane(lane).  No LDS traffic: the two
+// cross-row stages are gfx950 v_permlane32_swap / v_permlane16_swap (lanes
+// 32-63 of the first operand trade with lanes 0-31 of the second, resp. odd
+// with even rows), so after one swap of (v[j], v[j+h]) both halves hold
+// (own, partner) of the half they keep and a single add reduces it; the
+// in-row stages are DPP (row_ror:8 = lane ^ 8, row_shl/shr:4 = lane ^ 4,
+// quad_perm = lane ^ 2, lane ^ 1).
+__device__ __forceinline__ uint32_t dpp_xor4(uint32_t x, bool up) {
+  const uint32_t fwd = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xf, 0xf, false);  // row_shl:4 (lane + 4)
+  const uint32_t bwd = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xf, 0xf, false);  // row_shr:4 (lane - 4)
+  return up ? bwd : fwd;
+}
+
 __device__ __forceinline__ uint32_t reduce_scatter16(uint32_t (&v)[16]) {
   const int lane = lane_id();
-  {
-    const bool hi = lane & 32;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const uint32_t send = hi ? v[j] : v[j + 8];
-      const uint32_t keep = hi ? v[j + 8] : v[j];
-      v[j] = keep + (uint32_t)__shfl_xor((int)send, 32, 64);
-    }
+  for (int j = 0; j < 8; j++) {  // lane bit 5: keep objects j (low half) or j + 8
+    const auto r = __builtin_amdgcn_permlane32_swap(v[j], v[j + 8], false, false);
+    v[j] = r[0] + r[1];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {  // lane bit 4: keep j or j + 4
+    const auto r = __builtin_amdgcn_permlane16_swap(v[j], v[j + 4], false, false);
+    v[j] = r[0] + r[1];
   }
   {
-    const bool hi = lane & 16;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t send = hi ? v[j] : v[j + 4];
-      const uint32_t keep = hi ? v[j + 4] : v[j];
-      v[j] = keep + (uint32_t)__shfl_xor((int)send, 16, 64);
-    }
-  }
-  {
-    const bool hi = lane & 8;
+    const bool hi = lane & 8;  // row_ror:8 pairs lane with lane ^ 8
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const uint32_t send = hi ? v[j] : v[j + 2];
       const uint32_t keep = hi ? v[j + 2] : v[j];
-      v[j] = keep + (uint32_t)__shfl_xor((int)send, 8, 64);
+      v[j] = keep + (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0x128, 0xf, 0xf, false);
     }
   }
   {
     const bool hi = lane & 4;
     const uint32_t send = hi ? v[0] : v[1];
     const uint32_t keep = hi ? v[1] : v[0];
-    v[0] = keep + (uint32_t)__shfl_xor((int)send, 4, 64);
+    v[0] = keep + dpp_xor4(send, hi);
   }
   uint32_t r = v[0];
-  r += (uint32_t)__shfl_xor((int)r, 2, 64);
-  r += (uint32_t)__shfl_xor((int)r, 1, 64);
+  r += (uint32_t)__builtin_amdgcn_mov_dpp((int)r, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  r += (uint32_t)__builtin_amdgcn_mov_dpp((int)r, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
   return r;
 }
 
@@ -256,7 +264,7 @@ __device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* c
   const uint32_t nb = n == 0 ? 0 : (n - 1) / 16 + 1;
   const uint64_t blk = (uint64_t)8 * Me;
   // blocks whose loads are in flight together (bounded by VGPRs)
-  constexpr int NBF = PPL >= 4 ? 2 : (PPL == 2 ? 4 : 8);
+  constexpr int NBF = PPL >= 4 ? 1 : (PPL == 2 ? 2 : 4);
   for (uint32_t b0 = 0; b0 < nb; b0 += NBF) {
     uint4 c[NBF][PPL];
 #pragma unroll
@@ -389,6 +397,8 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
     bool bitmap_mode = !use_hash;
     uint32_t nvisited = 0, ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint64_t nadc = 0, nacc = 0, nexp = 0, nexact = 0, nblk = 0;
+    uint64_t t_pop = 0, t_ids = 0, t_adc = 0, t_acc = 0, t_last = 0;
+    (void)t_pop; (void)t_ids; (void)t_adc; (void)t_acc; (void)t_last;
     const uint32_t size = a.size;
     float radius = a.radius;
 
@@ -432,6 +442,9 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
     float expr = __fmul_rn(a.coef, radius);
 
     // ---- best-first loop over ADC distances (QuantizedGraph.h:220-268) ----
+#ifdef NGT_AMD_STAMPS
+    t_last = stamp();
+#endif
     for (;;) {
       uint64_t best = ~0ull;
       uint32_t bidx = 0xffffffffu;
@@ -455,6 +468,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       }
       if (bidx & 0x80000000u) nspill--; else ncq--;
       nexp++;
+      NGT_MARK(t_pop);
 
       // neighbour ids (0-terminated fixed-stride row) and their ADC distances
       const uint32_t target = key_id(wbest);
@@ -465,8 +479,10 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         st.nid[j + lane] = id;
         deg += (uint32_t)__popcll(ballot64(id != 0u));
       }
+      NGT_MARK(t_ids);
       adc_node<PPL>(L, a.qcodes + (uint64_t)target * a.code_stride, a.Me, deg, scale, toff, st.nd);
       __syncthreads();
+      NGT_MARK(t_adc);
       nadc += deg;
       nblk += deg == 0 ? 0 : (deg - 1) / 16 + 1;
 
@@ -523,6 +539,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
           __syncthreads();
         }
       }
+      NGT_MARK(t_acc);
     }
 
     // ---- results (QuantizedGraph.h:270-299) ------------------------------
@@ -571,6 +588,12 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         c[5] = maxq;
         c[6] = (bitmap_mode && use_hash) ? 1 : 0;
         c[7] = 0;
+#ifdef NGT_AMD_STAMPS
+        c[4] = t_pop;
+        c[5] = t_ids;
+        c[6] = t_adc;
+        c[7] = t_acc;
+#endif
       }
     }
     __syncthreads();

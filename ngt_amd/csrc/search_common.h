@@ -11,6 +11,27 @@
 
 namespace ngt_amd {
 
+// Diagnostic build only (-DNGT_AMD_STAMPS, libngt_amd_stamps.so): per-query
+// shader-clock totals of the search phases land in counters [5..7]; the
+// product build compiles these to nothing.
+#ifdef NGT_AMD_STAMPS
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define NGT_MARK(dst)              \
+  do {                             \
+    const uint64_t now_ = stamp(); \
+    dst += now_ - t_last;          \
+    t_last = now_;                 \
+  } while (0)
+#else
+#define NGT_MARK(dst)
+#endif
+
 template <typename T>
 __device__ __forceinline__ const T* row_ptr(const uint8_t* rows, uint64_t row_bytes, uint32_t id) {
   return reinterpret_cast<const T*>(rows + (uint64_t)id * row_bytes);
