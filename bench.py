@@ -233,6 +233,7 @@ def main():
     ap.add_argument("--qg-edges", type=int, default=128, help="NGTQG max edges per node")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
     ap.add_argument("--visited", type=int, default=-1,
                     help="visited set: -1 HBM epochs (C2 visits ~1e5 ids/query), 0 LDS hash")
     args = ap.parse_args()
@@ -311,10 +312,15 @@ def main():
     seeds = random_seeds(N + 1, NQ, args.seed_size)
     d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
     d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * args.seed_size
-    out_i = torch.zeros((NQ, K), dtype=torch.int32, device=dev)
-    out_d = torch.zeros((NQ, K), dtype=torch.float32, device=dev)
-    out_n = torch.zeros((NQ,), dtype=torch.int32, device=dev)
-    cnt = torch.zeros((NQ, COUNTERS), dtype=torch.int64, device=dev)
+    # consecutive steps alternate over `--streams` HIP streams (each with its
+    # own output buffers and, inside the library, its own launch scratch), so
+    # a step's kernel starts while the previous step's last queries drain
+    nstreams = 1 if shard else max(1, args.streams)
+    streams = [stream] + [torch.cuda.Stream(dev).cuda_stream for _ in range(nstreams - 1)]
+    bufs = [(torch.zeros((NQ, K), dtype=torch.int32, device=dev), torch.zeros((NQ, K), dtype=torch.float32, device=dev),
+             torch.zeros((NQ,), dtype=torch.int32, device=dev), torch.zeros((NQ, COUNTERS), dtype=torch.int64, device=dev))
+            for _ in range(nstreams)]
+    out_i, out_d, out_n, cnt = bufs[0]
     result = {"ids": out_i}
 
     if args.mode == "qg":
@@ -327,16 +333,17 @@ def main():
         del codes
         log("quantizer + quantized graph in %.1f s (degree <= %d)" % (time.time() - t0, ix.qg_max_degree()))
 
-    def run(eps):
+    def run(eps, si=0):
+        oi, od, on, oc = bufs[si]
         if args.mode == "qg":
-            ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, out_i.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
-                                cnt.data_ptr(), k=K, epsilon=eps, result_expansion=args.expansion,
+            ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                                oc.data_ptr(), k=K, epsilon=eps, result_expansion=args.expansion,
                                 seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
-                                stream=stream, visited_hash_log2=args.visited)
+                                stream=streams[si], visited_hash_log2=args.visited)
             return
-        ix.search_device(qdev.data_ptr(), dp * 4, NQ, out_i.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
-                         cnt.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
-                         d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=stream,
+        ix.search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                         oc.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
+                         d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=streams[si],
                          visited_hash_log2=args.visited)
         if shard:
             result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
@@ -360,15 +367,15 @@ def main():
         chosen = float(t.item())
         rec = measure(chosen)
 
-    for _ in range(args.warmup):
-        run(chosen)
+    for i in range(max(args.warmup, nstreams)):
+        run(chosen, i % nstreams)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run(chosen)
+    for i in range(args.steps):
+        run(chosen, i % nstreams)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -450,7 +457,8 @@ def main():
                        "distance_computations_per_query": float(c[:, 0].mean()),
                        "expansions_per_query": float(c[:, 2].mean()),
                        "visited_set": "hbm-epochs" if args.visited < 0 else "lds-hash",
-                       "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world)},
+                       "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world),
+                       "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes},

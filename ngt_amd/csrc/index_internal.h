@@ -60,8 +60,26 @@ struct QgState {
   uint32_t id_stride = 0;
   uint64_t code_stride = 0;
   bool has_graph = false;
-  DevBuf<uint8_t> lut;      // per-search scratch: [nq][Me*16]
+};
+
+// Scratch owned by one in-flight search launch.  One context per HIP stream
+// a caller searches on, so consecutive batches on different streams run
+// concurrently (the next batch's waves fill the CUs the previous batch's
+// tail leaves idle) without sharing visited arrays or work counters.
+struct SearchCtx {
+  hipStream_t stream = nullptr;
+  DevBuf<uint32_t> work, seeds, seed_count, slot_epoch;
+  DevBuf<uint64_t> seed_off, spill;
+  DevBuf<uint8_t> vis;           // [slots][vis_stride] visited epochs
+  uint32_t slots = 0;
+  uint64_t vis_stride = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the search kernel
+  DevBuf<uint8_t> lut;           // NGTQG: [nq][Me*16]
   DevBuf<float> scale, toff;
+  ~SearchCtx() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+  }
 };
 
 }  // namespace ngt_amd
@@ -100,16 +118,14 @@ struct ngt_amd_index {
   int32_t dyn_base = 30, dyn_rate = 20;
   int32_t seed_size = 10, seed_type = 0;
   // scratch
-  DevBuf<uint32_t> work, seeds, seed_count, slot_epoch;
-  DevBuf<uint8_t> vis;
-  DevBuf<uint64_t> spill, seed_off;
+  std::vector<ngt_amd::SearchCtx*> ctxs;   // per launch stream
+  ngt_amd::SearchCtx* last_ctx = nullptr;  // context of the latest search
   DevBuf<int> error;
-  uint32_t slots = 0;
-  uint64_t vis_stride = 0;
   uint32_t spill_cap = 1u << 16;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  float last_ms = 0.f;
+  ~ngt_amd_index() {
+    for (auto* c : ctxs) delete c;
+  }
   int cu_count = 256;
   size_t lds_per_cu = 160 * 1024;
   QgState qg;                      // NGTQG quantized graph (qg_api.cpp)
@@ -119,9 +135,11 @@ namespace ngt_amd {
 
 constexpr uint32_t kTreeSeedStride = 128;  // max seeds per query from a tree leaf
 
-int ensure_vis_scratch(ngt_amd_index* ix, size_t lds_per_slot, hipStream_t s);
-int run_tree_seeds(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq, uint32_t k,
-                   int all_leaf_nodes, hipStream_t s);
+// the launch context of stream s (created on first use), or null on failure
+SearchCtx* ctx_for(ngt_amd_index* ix, hipStream_t s);
+int ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds_per_slot, hipStream_t s);
+int run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queries, uint64_t query_bytes, uint32_t nq,
+                   uint32_t k, int all_leaf_nodes, hipStream_t s);
 float coef_of(float epsilon);
 // GraphIndex::getRandomSeeds (Index.h:775-801) over the process rand() stream
 std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off);

@@ -73,12 +73,11 @@ extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distanc
   ix->row_bytes = (uint64_t)ix->dp * ix->esize;
   ix->cu_count = prop.multiProcessorCount;
   ix->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
-  if (hipStreamCreateWithFlags(&ix->stream, hipStreamDefault) != hipSuccess ||
-      hipEventCreate(&ix->ev0) != hipSuccess || hipEventCreate(&ix->ev1) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&ix->stream, hipStreamDefault) != hipSuccess) {
     delete ix;
     return fail("ngt_amd_index_create: stream/event creation failed");
   }
-  if (ix->error.alloc(1) != hipSuccess || ix->work.alloc(4) != hipSuccess) {
+  if (ix->error.alloc(1) != hipSuccess) {
     delete ix;
     return fail("ngt_amd_index_create: allocation failed");
   }
@@ -91,8 +90,6 @@ extern "C" void ngt_amd_index_destroy(ngt_amd_index* ix) {
   if (!ix) return;
   (void)hipSetDevice(ix->device);
   if (ix->stream) (void)hipStreamSynchronize(ix->stream);
-  if (ix->ev0) (void)hipEventDestroy(ix->ev0);
-  if (ix->ev1) (void)hipEventDestroy(ix->ev1);
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
   delete ix;
 }
@@ -239,7 +236,22 @@ extern "C" uint64_t ngt_amd_resolve_edge_size(const ngt_amd_index* ix, int64_t e
 // Per-slot scratch of the persistent search kernels (slot = resident wave):
 // visited-epoch bytes, their epochs and the unchecked-set spill.  Sized by the
 // LDS footprint of one slot, which bounds how many are resident per CU.
-int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, size_t lds, hipStream_t s) {
+ngt_amd::SearchCtx* ngt_amd::ctx_for(ngt_amd_index* ix, hipStream_t s) {
+  for (auto* c : ix->ctxs)
+    if (c->stream == s) return ix->last_ctx = c;
+  auto* c = new SearchCtx();
+  c->stream = s;
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      c->work.alloc(4) != hipSuccess) {
+    delete c;
+    fail("search: cannot create the launch context of stream %p", (void*)s);
+    return nullptr;
+  }
+  ix->ctxs.push_back(c);
+  return ix->last_ctx = c;
+}
+
+int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds, hipStream_t s) {
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
   if (per_cu > 16) per_cu = 16;
   if (per_cu < 1) per_cu = 1;
@@ -247,27 +259,27 @@ int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, size_t lds, hipStream_t s) {
   // the per-slot visited epochs take slots * nrows bytes: keep them <= 16 GiB
   uint64_t max_slots = (16ull << 30) / stride;
   uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * ix->cu_count, std::max<uint64_t>(max_slots, 64));
-  if (slots != ix->slots || stride != ix->vis_stride || !ix->spill.p) {
-    HIP_OK(ix->vis.alloc((size_t)slots * stride));
+  if (slots != c->slots || stride != c->vis_stride || !c->spill.p) {
+    HIP_OK(c->vis.alloc((size_t)slots * stride));
     // zeroed on the launch stream so the first search is ordered after it
-    HIP_OK(hipMemsetAsync(ix->vis.p, 0, (size_t)slots * stride, s));
-    HIP_OK(ix->slot_epoch.alloc(slots));
-    HIP_OK(hipMemsetAsync(ix->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t), s));
-    HIP_OK(ix->spill.alloc((size_t)slots * ix->spill_cap));
-    ix->slots = slots;
-    ix->vis_stride = stride;
+    HIP_OK(hipMemsetAsync(c->vis.p, 0, (size_t)slots * stride, s));
+    HIP_OK(c->slot_epoch.alloc(slots));
+    HIP_OK(hipMemsetAsync(c->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t), s));
+    HIP_OK(c->spill.alloc((size_t)slots * ix->spill_cap));
+    c->slots = slots;
+    c->vis_stride = stride;
   }
   return 0;
 }
 
 // GraphAndTreeIndex::getSeedsFromTree (Index.h:1524-1567) for a batch: seed
-// lists land in ix->seeds ([nq][kTreeSeedStride]) and ix->seed_count.
-int ngt_amd::run_tree_seeds(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq,
-                            uint32_t k, int all_leaf_nodes, hipStream_t s) {
+// lists land in c->seeds ([nq][kTreeSeedStride]) and c->seed_count.
+int ngt_amd::run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queries, uint64_t query_bytes,
+                            uint32_t nq, uint32_t k, int all_leaf_nodes, hipStream_t s) {
   if (!ix->has_tree) return fail("search: tree seeds requested but the index has no tree");
   const uint32_t stride = kTreeSeedStride;
-  HIP_OK(ix->seeds.alloc((size_t)nq * stride));
-  HIP_OK(ix->seed_count.alloc(nq));
+  HIP_OK(c->seeds.alloc((size_t)nq * stride));
+  HIP_OK(c->seed_count.alloc(nq));
   TreeSeedArgs t{};
   t.queries = static_cast<const uint8_t*>(d_queries);
   t.query_bytes = query_bytes;
@@ -284,14 +296,14 @@ int ngt_amd::run_tree_seeds(ngt_amd_index* ix, const void* d_queries, uint64_t q
   t.seed_size = (uint32_t)std::max(ix->seed_size, 0);
   t.k = k;
   t.all_leaf_nodes = all_leaf_nodes || ix->seed_type == 4;
-  t.seeds = ix->seeds.p;
+  t.seeds = c->seeds.p;
   t.seed_stride = stride;
-  t.seed_count = ix->seed_count.p;
+  t.seed_count = c->seed_count.p;
   HIP_OK(launch_tree_seeds(t, ix->metric, ix->otype, s));
   return 0;
 }
 
-static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const void* d_queries,
+static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_params* prm, const void* d_queries,
                       uint64_t query_bytes, uint32_t nq, const uint32_t* d_seeds,
                       const uint64_t* d_seed_off, uint32_t* d_ids, float* d_dists, uint32_t* d_n,
                       uint64_t* d_counters, hipStream_t s) {
@@ -334,10 +346,10 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
   a.error = ix->error.p;
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
-    if (run_tree_seeds(ix, d_queries, query_bytes, nq, prm->k, prm->all_leaf_nodes, s)) return -1;
-    a.seeds = ix->seeds.p;
+    if (run_tree_seeds(ix, c, d_queries, query_bytes, nq, prm->k, prm->all_leaf_nodes, s)) return -1;
+    a.seeds = c->seeds.p;
     a.seed_stride = kTreeSeedStride;
-    a.seed_count = ix->seed_count.p;
+    a.seed_count = c->seed_count.p;
   } else {
     if (!d_seeds || !d_seed_off) return fail("search: seed lists required for this seed mode");
     a.seeds = d_seeds;
@@ -345,18 +357,18 @@ static int run_search(ngt_amd_index* ix, const ngt_amd_search_params* prm, const
   }
   const size_t lds = search_lds_bytes(a, ix->otype);
   if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
-  if (ensure_vis_scratch(ix, lds, s)) return -1;
-  a.vis = ix->vis.p;
-  a.vis_stride = ix->vis_stride;
-  a.slot_epoch = ix->slot_epoch.p;
-  a.spill = ix->spill.p;
+  if (ensure_vis_scratch(ix, c, lds, s)) return -1;
+  a.vis = c->vis.p;
+  a.vis_stride = c->vis_stride;
+  a.slot_epoch = c->slot_epoch.p;
+  a.spill = c->spill.p;
   a.spill_cap = ix->spill_cap;
-  a.work = ix->work.p;
-  HIP_OK(hipMemsetAsync(ix->work.p, 0, sizeof(uint32_t), s));
-  uint32_t slots = std::min<uint32_t>(ix->slots, nq);
-  HIP_OK(hipEventRecord(ix->ev0, s));
+  a.work = c->work.p;
+  HIP_OK(hipMemsetAsync(c->work.p, 0, sizeof(uint32_t), s));
+  uint32_t slots = std::min<uint32_t>(c->slots, nq);
+  HIP_OK(hipEventRecord(c->ev0, s));
   HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
-  HIP_OK(hipEventRecord(ix->ev1, s));
+  HIP_OK(hipEventRecord(c->ev1, s));
   return 0;
 }
 
@@ -394,22 +406,25 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
   hipStream_t s = (hipStream_t)stream;  // null = the default stream
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
   if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
     std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
-    HIP_OK(ix->seed_off.upload(off.data(), off.size()));
-    HIP_OK(ix->seeds.upload(seeds.data(), seeds.size()));
-    return run_search(ix, prm, d_queries, query_bytes, nq, ix->seeds.p, ix->seed_off.p, d_ids,
+    HIP_OK(c->seed_off.upload(off.data(), off.size()));
+    HIP_OK(c->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
+    return run_search(ix, c, prm, d_queries, query_bytes, nq, c->seeds.p, c->seed_off.p, d_ids,
                       d_dists, d_n, d_counters, s);
   }
-  return run_search(ix, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, d_ids, d_dists,
+  return run_search(ix, c, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, d_ids, d_dists,
                     d_n, d_counters, s);
 }
 
 extern "C" float ngt_amd_last_search_kernel_ms(const ngt_amd_index* ix) {
   if (!ix) return 0.f;
+  if (!ix->last_ctx) return -1.f;
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, ix->ev0, ix->ev1) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, ix->last_ctx->ev0, ix->last_ctx->ev1) != hipSuccess) return -1.f;
   return ms;
 }
 

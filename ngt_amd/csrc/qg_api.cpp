@@ -140,12 +140,13 @@ extern "C" int ngt_amd_qg_get_graph(const ngt_amd_index* ix, uint32_t* ids, uint
   return 0;
 }
 
-// LUTs of nq prepared device queries into ix->qg.lut/scale/toff.
-static int run_lut(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq, hipStream_t s) {
+// LUTs of nq prepared device queries into c->lut/scale/toff.
+static int run_lut(ngt_amd_index* ix, SearchCtx* c, const void* d_queries, uint64_t query_bytes, uint32_t nq,
+                   hipStream_t s) {
   QgState& q = ix->qg;
-  HIP_OK(q.lut.alloc((size_t)nq * q.Me * 16));
-  HIP_OK(q.scale.alloc(nq));
-  HIP_OK(q.toff.alloc(nq));
+  HIP_OK(c->lut.alloc((size_t)nq * q.Me * 16));
+  HIP_OK(c->scale.alloc(nq));
+  HIP_OK(c->toff.alloc(nq));
   QgLutArgs a{};
   a.queries = static_cast<const uint8_t*>(d_queries);
   a.query_bytes = query_bytes;
@@ -155,10 +156,10 @@ static int run_lut(ngt_amd_index* ix, const void* d_queries, uint64_t query_byte
   a.M = q.M;
   a.dsub = q.dsub;
   a.Me = q.Me;
-  a.lut = q.lut.p;
+  a.lut = c->lut.p;
   a.lut_stride = (uint64_t)q.Me * 16;
-  a.scale = q.scale.p;
-  a.toff = q.toff.p;
+  a.scale = c->scale.p;
+  a.toff = c->toff.p;
   HIP_OK(launch_qg_lut(a, s));
   return 0;
 }
@@ -173,11 +174,13 @@ extern "C" int ngt_amd_qg_lut(ngt_amd_index* ix, const float* queries, uint32_t 
   DevBuf<float> raw;
   DevBuf<uint8_t> prep;
   if (upload_queries(ix, queries, nq, raw, prep, s)) return -1;
-  if (run_lut(ix, prep.p, ix->row_bytes, nq, s)) return -1;
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
+  if (run_lut(ix, c, prep.p, ix->row_bytes, nq, s)) return -1;
   const QgState& q = ix->qg;
-  HIP_OK(hipMemcpyAsync(lut, q.lut.p, (size_t)nq * q.Me * 16, hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(scale, q.scale.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(total_offset, q.toff.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(lut, c->lut.p, (size_t)nq * q.Me * 16, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(scale, c->scale.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(total_offset, c->toff.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return 0;
 }
@@ -241,6 +244,8 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   HIP_OK(hipSetDevice(ix->device));
   hipStream_t s = (hipStream_t)stream;
   QgState& q = ix->qg;
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
 
   QgSearchArgs a{};
   a.rows = ix->rows.p;
@@ -278,43 +283,43 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
     // getSeedsFromTree with the caller's k (before the expansion, :362)
-    if (run_tree_seeds(ix, d_queries, query_bytes, nq, prm->k, 0, s)) return -1;
-    a.seeds = ix->seeds.p;
+    if (run_tree_seeds(ix, c, d_queries, query_bytes, nq, prm->k, 0, s)) return -1;
+    a.seeds = c->seeds.p;
     a.seed_stride = kTreeSeedStride;
-    a.seed_count = ix->seed_count.p;
+    a.seed_count = c->seed_count.p;
   } else if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
     std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
-    HIP_OK(ix->seed_off.upload(off.data(), off.size()));
-    HIP_OK(ix->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
-    a.seeds = ix->seeds.p;
-    a.seed_off = ix->seed_off.p;
+    HIP_OK(c->seed_off.upload(off.data(), off.size()));
+    HIP_OK(c->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
+    a.seeds = c->seeds.p;
+    a.seed_off = c->seed_off.p;
   } else {
     if (!d_seeds || !d_seed_off) return fail("ngt_amd_qg_search: seed lists required for this seed mode");
     a.seeds = d_seeds;
     a.seed_off = d_seed_off;
   }
-  if (run_lut(ix, d_queries, query_bytes, nq, s)) return -1;
-  a.lut = q.lut.p;
+  if (run_lut(ix, c, d_queries, query_bytes, nq, s)) return -1;
+  a.lut = c->lut.p;
   a.lut_stride = (uint64_t)q.Me * 16;
-  a.scale = q.scale.p;
-  a.toff = q.toff.p;
+  a.scale = c->scale.p;
+  a.toff = c->toff.p;
 
   const size_t lds = qg_search_lds_bytes(a);
   if (lds > 64 * 1024)
     return fail("ngt_amd_qg_search: k=%u x expansion needs %zu bytes of LDS per query (max 65536)", a.k, lds);
-  if (ensure_vis_scratch(ix, lds, s)) return -1;
-  a.vis = ix->vis.p;
-  a.vis_stride = ix->vis_stride;
-  a.slot_epoch = ix->slot_epoch.p;
-  a.spill = ix->spill.p;
+  if (ensure_vis_scratch(ix, c, lds, s)) return -1;
+  a.vis = c->vis.p;
+  a.vis_stride = c->vis_stride;
+  a.slot_epoch = c->slot_epoch.p;
+  a.spill = c->spill.p;
   a.spill_cap = ix->spill_cap;
-  a.work = ix->work.p;
-  HIP_OK(hipMemsetAsync(ix->work.p, 0, sizeof(uint32_t), s));
-  const uint32_t slots = std::min<uint32_t>(ix->slots, nq);
-  HIP_OK(hipEventRecord(ix->ev0, s));
+  a.work = c->work.p;
+  HIP_OK(hipMemsetAsync(c->work.p, 0, sizeof(uint32_t), s));
+  const uint32_t slots = std::min<uint32_t>(c->slots, nq);
+  HIP_OK(hipEventRecord(c->ev0, s));
   HIP_OK(launch_qg_search(a, slots, s));
-  HIP_OK(hipEventRecord(ix->ev1, s));
+  HIP_OK(hipEventRecord(c->ev1, s));
   return 0;
 }
 

@@ -317,3 +317,45 @@ def test_device_api_first_launch_exact():
         assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od_.view(np.uint32))
         assert int(cnt[i, 0]) == int(ocnt[0])
     ix.close()
+
+
+def test_concurrent_streams_exact():
+    """Searches on two HIP streams run concurrently, each with its own launch
+    scratch (visited epochs, work counter): results equal the sequential run
+    and the oracle."""
+    import torch
+    n, dim, deg, nq = 30000, 32, 24, 512
+    rows, offs, edges = _random_graph(n, dim, deg, 33)
+    dev = torch.device("cuda:0")
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(12)
+    qs = rng.random((2, nq, dim), dtype=np.float32)
+    seeds = np.stack([rng.choice(np.arange(1, n), 10, replace=False) for _ in range(nq)]).astype(np.uint32)
+    d_s = torch.from_numpy(seeds.reshape(-1).view(np.int32)).to(dev)
+    d_o = torch.arange(0, nq + 1, dtype=torch.int64, device=dev) * 10
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = []
+    for b in range(2):
+        d_q = torch.from_numpy(qs[b]).to(dev)
+        oi = torch.zeros((nq, 10), dtype=torch.int32, device=dev)
+        od = torch.zeros((nq, 10), dtype=torch.float32, device=dev)
+        on = torch.zeros((nq,), dtype=torch.int32, device=dev)
+        outs.append((d_q, oi, od, on))
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for b in range(2):
+            d_q, oi, od, on = outs[b]
+            ix.search_device(d_q.data_ptr(), dim * 4, nq, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None, k=10,
+                             epsilon=0.3, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_s.data_ptr(),
+                             d_seed_off=d_o.data_ptr(), stream=streams[b].cuda_stream, visited_hash_log2=-1)
+    torch.cuda.synchronize()
+    for b in range(2):
+        _, oi, od, on = outs[b]
+        gi, gd, gn = oi.cpu().numpy().view(np.uint32), od.cpu().numpy(), on.cpu().numpy()
+        for i in range(0, nq, 8):
+            oid, od_, _ = O.search("l2", rows, offs, edges, qs[b][i], seeds[i], 10, np.float32(0.3))
+            assert list(gi[i, :gn[i]]) == list(oid), (b, i)
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od_.view(np.uint32))
+    ix.close()
