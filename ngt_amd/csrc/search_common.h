@@ -206,4 +206,88 @@ __device__ __forceinline__ void eval_l2f_fast(const float* qlds, const uint8_t* 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Long rows (Dp > 128, Dp/16 a multiple of 4; C3: 960 floats = 3,840 B):
+// streamed through registers in stages of 4 float4 per lane with the next
+// stage's loads issued before the current stage's FMAs, so a 16-row wave
+// step keeps 16 rows x 256 B per lane group in flight instead of waiting on
+// each unrolled chunk.  Same quad mapping and per-lane FMA order over the
+// chunks as dist_f32 (chunk i strictly in order), hence bit-identical.
+// Cosine/angle: the query's sum of squares (compareCosine's first
+// accumulator, PrimitiveComparator.h:487-553) depends on the query only, so
+// it is folded once per query (query_sq_fold) and reused.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float query_sq_fold(const float* qlds, int dp) {
+  const int g = lane_id() & 3;
+  const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
+  float4 na = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < (dp >> 4); i++) {
+    const float4 qv = qq[4 * i];
+    na.x = __builtin_fmaf(qv.x, qv.x, na.x); na.y = __builtin_fmaf(qv.y, qv.y, na.y);
+    na.z = __builtin_fmaf(qv.z, qv.z, na.z); na.w = __builtin_fmaf(qv.w, qv.w, na.w);
+  }
+  return fold16(na);
+}
+
+template <int M>
+__device__ __forceinline__ void stream_stage(const float4* qq, int c, const float4 (&b)[4], float4& a0, float4& a1) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const float4 qv = qq[4 * (c + k)];
+    const float4 xv = b[k];
+    if constexpr (M == kL2) {
+      const float vx = qv.x - xv.x, vy = qv.y - xv.y, vz = qv.z - xv.z, vw = qv.w - xv.w;
+      a0.x = __builtin_fmaf(vx, vx, a0.x); a0.y = __builtin_fmaf(vy, vy, a0.y);
+      a0.z = __builtin_fmaf(vz, vz, a0.z); a0.w = __builtin_fmaf(vw, vw, a0.w);
+    } else {  // kCosine / kAngle: a0 = sum x^2, a1 = sum x*q
+      a0.x = __builtin_fmaf(xv.x, xv.x, a0.x); a0.y = __builtin_fmaf(xv.y, xv.y, a0.y);
+      a0.z = __builtin_fmaf(xv.z, xv.z, a0.z); a0.w = __builtin_fmaf(xv.w, xv.w, a0.w);
+      a1.x = __builtin_fmaf(xv.x, qv.x, a1.x); a1.y = __builtin_fmaf(xv.y, qv.y, a1.y);
+      a1.z = __builtin_fmaf(xv.z, qv.z, a1.z); a1.w = __builtin_fmaf(xv.w, qv.w, a1.w);
+    }
+  }
+}
+
+template <int M>
+__device__ __forceinline__ void eval_stream(const float* qlds, const uint8_t* rows, uint64_t row_bytes, int dp,
+                                            float qfold, const uint32_t* ids, float* dists, int m) {
+  const int lane = lane_id();
+  const int g = lane & 3, rs = lane >> 2;
+  const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
+  const int nch = dp >> 4;  // float4 per lane, a multiple of 4
+  for (int r0 = 0; r0 < m; r0 += 16) {
+    const int r = r0 + rs;
+    const uint32_t id = r < m ? ids[r] : 0u;  // out-of-range lanes read the dummy row
+    const float4* x = reinterpret_cast<const float4*>(rows + (uint64_t)id * row_bytes) + g;
+    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+    float4 b0[4], b1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) b0[k] = x[4 * k];
+    for (int c = 0; c < nch; c += 8) {
+      const bool more = c + 4 < nch;
+      if (more) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) b1[k] = x[4 * (c + 4 + k)];
+      }
+      stream_stage<M>(qq, c, b0, a0, a1);
+      if (!more) break;
+      if (c + 8 < nch) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) b0[k] = x[4 * (c + 8 + k)];
+      }
+      stream_stage<M>(qq, c + 4, b1, a0, a1);
+    }
+    float d;
+    if constexpr (M == kL2) {
+      d = (float)sqrt((double)fold16(a0));
+    } else {
+      const double dnb = fold16(a0), ds = fold16(a1);
+      const double cs = ds / sqrt((double)qfold * dnb);
+      if constexpr (M == kCosine) d = (float)(1.0 - cs);
+      else d = (float)angle_of(cs);
+    }
+    if (g == 0 && r < m) dists[r] = d;
+  }
+}
+
 }  // namespace ngt_amd

@@ -138,18 +138,23 @@ __global__ void __launch_bounds__(64) ngt_tree_seed_kernel(TreeSeedArgs a) {
 // Graph search.
 // ---------------------------------------------------------------------------
 
+// NCH > 0: L2 over float rows of exactly 16*NCH elements held in registers;
+// NCH == -1: long float rows streamed in stages (eval_stream, L2/cosine/angle);
+// NCH == 0: the generic comparator of any metric.
 template <int M, typename T, int NCH, int G>
-__device__ __forceinline__ void eval_any(const T* qlds, const SearchArgs& a, const uint32_t* ids, float* dists,
-                                         int m) {
+__device__ __forceinline__ void eval_any(const T* qlds, const SearchArgs& a, float qfold, const uint32_t* ids,
+                                         float* dists, int m) {
   if constexpr (NCH > 0 && M == kL2 && sizeof(T) == 4) {
     eval_l2f_fast<NCH, G>(reinterpret_cast<const float*>(qlds), a.rows, a.row_bytes, ids, dists, m);
+  } else if constexpr (NCH < 0 && sizeof(T) == 4) {
+    eval_stream<M>(reinterpret_cast<const float*>(qlds), a.rows, a.row_bytes, a.dp, qfold, ids, dists, m);
   } else {
     eval_batch<M, T>(qlds, a.rows, a.row_bytes, a.dp, ids, dists, m);
   }
 }
 
 template <int M, typename T, int NCH, int G>
-__global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
+__global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = lane_id();
   SearchState st;
@@ -191,6 +196,9 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
     }
     __syncthreads();
     if (lane == 0) a.slot_epoch[slot] = epoch;
+    float qfold = 0.f;
+    if constexpr (NCH < 0 && (M == kCosine || M == kAngle))
+      qfold = query_sq_fold(reinterpret_cast<const float*>(qlds), a.dp);
 
     bool bitmap_mode = !use_hash;
     uint32_t nvisited = 0;
@@ -211,7 +219,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
       const uint32_t m = ns - base < 64 ? ns - base : 64;
       if ((uint32_t)lane < m) st.nid[lane] = a.seeds[sb + base + lane];
       __syncthreads();
-      eval_any<M, T, NCH, G>(qlds, a, st.nid, st.nd, (int)m);
+      eval_any<M, T, NCH, G>(qlds, a, qfold, st.nid, st.nd, (int)m);
       __syncthreads();
       if ((uint32_t)lane < m) {
         const uint32_t id = st.nid[lane];
@@ -300,7 +308,7 @@ __global__ void __launch_bounds__(64, (NCH > 0 && G == 1) ? 4 : 2) ngt_graph_sea
         __syncthreads();
         NGT_MARK(t_adj);
         if (m != 0) {
-          eval_any<M, T, NCH, G>(qlds, a, st.nid, st.nd, (int)m);
+          eval_any<M, T, NCH, G>(qlds, a, qfold, st.nid, st.nd, (int)m);
           __syncthreads();
           NGT_MARK(t_eval);
           ndist += m;
@@ -579,6 +587,21 @@ hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint3
     else
       hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 6, 1>), dim3(slots), dim3(64), lds, s, a);
     return hipGetLastError();
+  }
+  // long float rows: streamed comparator (C3: 960-d cosine)
+  if (otype == kFloat && a.dp > 128 && ((a.dp >> 4) & 3) == 0 && !getenv("NGT_AMD_NO_STREAM")) {
+    if (metric == kL2) {
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, -1, 1>), dim3(slots), dim3(64), lds, s, a);
+      return hipGetLastError();
+    }
+    if (metric == kCosine) {
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kCosine, float, -1, 1>), dim3(slots), dim3(64), lds, s, a);
+      return hipGetLastError();
+    }
+    if (metric == kAngle) {
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kAngle, float, -1, 1>), dim3(slots), dim3(64), lds, s, a);
+      return hipGetLastError();
+    }
   }
 #define L_SEARCH(MM, TT) hipLaunchKernelGGL((ngt_graph_search_kernel<MM, TT, 0, 1>), dim3(slots), dim3(64), lds, s, a)
   NGT_DISPATCH(metric, otype, L_SEARCH);

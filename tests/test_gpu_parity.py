@@ -359,3 +359,32 @@ def test_concurrent_streams_exact():
             assert list(gi[i, :gn[i]]) == list(oid), (b, i)
             assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od_.view(np.uint32))
     ix.close()
+
+
+@pytest.mark.parametrize("metric", ["l2", "cosine", "angle"])
+@pytest.mark.parametrize("dim", [256, 960, 200])
+def test_long_rows_stream_exact(metric, dim):
+    """Long float rows take the streamed comparator (Dp/16 a multiple of 4:
+    256, 960; 200 -> Dp 208 stays on the generic one): same ids, bit-exact
+    distances and the same work as the restatement."""
+    n, deg, nq = 2500, 16, 24
+    rows, offs, edges = _random_graph(n, dim, deg, 17)
+    ix = DeviceIndex(metric, "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(6)
+    qs = rng.random((nq, dim), dtype=np.float32)
+    seeds = [rng.choice(np.arange(1, n), 10, replace=False).astype(np.uint32) for _ in range(nq)]
+    gi, gd, gn, cnt = ix.search(qs, k=10, epsilon=0.2, edge_size=0, seed_mode=SEED_GIVEN, seeds=seeds,
+                                visited_hash_log2=-1)
+    dp = ((dim - 1) // 16 + 1) * 16
+    rp = np.zeros((n, dp), np.float32)
+    rp[:, :dim] = rows
+    for i in range(nq):
+        q = np.zeros(dp, np.float32)
+        q[:dim] = qs[i]
+        oid, od, ocnt = O.search(metric, rp, offs, edges, q, seeds[i], 10, np.float32(0.2))
+        assert list(gi[i, :gn[i]]) == list(oid), (metric, dim, i)
+        assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32)), (metric, dim, i)
+        assert int(cnt[i, 0]) == int(ocnt[0])
+    ix.close()
