@@ -159,6 +159,47 @@ int ngt_amd_prepare_queries_device(ngt_amd_index *index, const float *d_in, uint
 /* Timing of the last search call's kernels (HIP events on the search stream), ms. */
 float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
 
+/* ---- ANNG construction --------------------------------------------------- *
+ *   ngt_amd_build_begin / _insert <- GraphAndTreeIndex::createIndex(threadPoolSize)
+ *   (lib/NGT/Index.cpp:1158-1257) for graphType ANNG (truncation disabled, the
+ *   default): per batch of batch_size_for_creation objects in id order, the
+ *   insertion searches (searchForNNGInsertion, Index.h:1457-1479: DVP-tree
+ *   seeds with useAllNodesInLeaf, size edgeSizeForCreation, coefficient
+ *   epsilon_for_creation + 1), the batch's pairwise distances and merge
+ *   (insertMultipleSearchResults, Index.cpp:673-727), insertANNGNode
+ *   (Graph.h:611-625) and DVPTree::insert (Tree.cpp:27-265).  The objects must
+ *   be set first (ngt_amd_index_set_objects); the index's search graph is
+ *   replaced by the construction's padded adjacency until the built graph is
+ *   set back with ngt_amd_index_set_graph. */
+typedef struct {
+  int32_t edge_size_for_creation;   /* EdgeSizeForCreation (10)                      */
+  int32_t edge_size_for_search;     /* EdgeSizeForSearch (40), <= 256; 0 = all edges */
+  int32_t batch_size_for_creation;  /* BatchSizeForCreation (200)                    */
+  int32_t seed_size;                /* SeedSize (10)                                 */
+  float epsilon_for_creation;       /* EpsilonForCreation (0.1)                      */
+  int32_t reserved;
+} ngt_amd_build_params;
+
+int ngt_amd_build_begin(ngt_amd_index *index, const ngt_amd_build_params *params);
+/* Insert the valid objects with ids in [first_id, end_id) not yet in the graph. */
+int ngt_amd_build_insert(ngt_amd_index *index, uint64_t first_id, uint64_t end_id);
+/* GraphRepository size (max inserted id + 1) and total edge count. */
+int ngt_amd_build_graph_size(const ngt_amd_index *index, uint64_t *graph_size, uint64_t *nedges);
+/* CSR of the built graph: node v's edges ids/dists[offsets[v] .. offsets[v+1]),
+ * sorted by (distance, id); offsets [graph_size + 1]. */
+int ngt_amd_build_get_graph(const ngt_amd_index *index, uint64_t *offsets, uint32_t *ids, float *dists);
+/* Node-slot counts of the built DVP tree (slot 0 of each is the unused dummy)
+ * and the total number of leaf entries. */
+int ngt_amd_build_tree_size(const ngt_amd_index *index, uint32_t *n_leaf, uint32_t *n_internal,
+                            uint64_t *n_leaf_ids);
+/* The built DVP tree (Node.h:90-480 fields): per leaf slot parent (raw
+ * Node::ID), objects (id, distance) at leaf_off, pivot row; per internal slot
+ * parent, pivot row, children[5] (raw ids), borders[4]. */
+int ngt_amd_build_get_tree(const ngt_amd_index *index, uint32_t *leaf_parent, uint64_t *leaf_off,
+                           uint32_t *leaf_ids, float *leaf_dists, uint8_t *leaf_has_pivot,
+                           void *leaf_pivot, uint32_t *in_parent, void *in_pivot, uint32_t *in_child,
+                           float *in_border);
+
 /* ---- repository sharding (one shard per GPU) ------------ *
  * Merge of per-shard result lists gathered from every rank (RCCL all-gather
  * over xGMI): the k best (distance, global id) per query, the ordering of

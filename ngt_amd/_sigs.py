@@ -14,6 +14,12 @@ class QgSearchParams(Structure):
                 ("seed_mode", c_int32), ("visited_hash_log2", c_int32)]
 
 
+class BuildParams(Structure):
+    _fields_ = [("edge_size_for_creation", c_int32), ("edge_size_for_search", c_int32),
+                ("batch_size_for_creation", c_int32), ("seed_size", c_int32), ("epsilon_for_creation", c_float),
+                ("reserved", c_int32)]
+
+
 class NGTQGQuery(Structure):
     _fields_ = [("query", POINTER(c_float)), ("size", c_size_t), ("epsilon", c_float),
                 ("result_expansion", c_float), ("radius", c_float)]
@@ -62,6 +68,12 @@ def declare(L):
         "ngt_amd_distances": (c_int, [vp, vp, c_uint32, vp, vp, c_uint64, vp]),
         "ngt_amd_prepare_queries_device": (c_int, [vp, vp, c_uint32, vp, vp]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
+        "ngt_amd_build_begin": (c_int, [vp, POINTER(BuildParams)]),
+        "ngt_amd_build_insert": (c_int, [vp, c_uint64, c_uint64]),
+        "ngt_amd_build_graph_size": (c_int, [vp, u64p, u64p]),
+        "ngt_amd_build_get_graph": (c_int, [vp, vp, vp, vp]),
+        "ngt_amd_build_tree_size": (c_int, [vp, u32p, u32p, u64p]),
+        "ngt_amd_build_get_tree": (c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "ngt_amd_merge_results_device": (c_int, [c_int, vp, vp, vp, c_uint32, c_uint32, c_uint32, vp, vp, vp, vp,
                                                  vp]),
         "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),

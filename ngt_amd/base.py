@@ -44,6 +44,54 @@ class Index(object):
         if not ok:
             raise NativeError(_err_string(self._L, err))
 
+    @staticmethod
+    def create(path, dimension, edge_size_for_creation=10, edge_size_for_search=40, object_type="Float",
+               distance_type="L2"):
+        """Create an empty index directory (python/ngt/base.py:199-279 ->
+        ngt_create_graph_and_tree)."""
+        L = lib()
+        err = L.ngt_create_error_object()
+        prop = L.ngt_create_property(err)
+        ok = L.ngt_set_property_dimension(prop, dimension, err) and \
+            L.ngt_set_property_edge_size_for_creation(prop, edge_size_for_creation, err) and \
+            L.ngt_set_property_edge_size_for_search(prop, edge_size_for_search, err)
+        ok = ok and (L.ngt_set_property_object_type_float(prop, err) if object_type == "Float"
+                     else L.ngt_set_property_object_type_integer(prop, err))
+        setters = {"L1": L.ngt_set_property_distance_type_l1, "L2": L.ngt_set_property_distance_type_l2,
+                   "Angle": L.ngt_set_property_distance_type_angle,
+                   "Hamming": L.ngt_set_property_distance_type_hamming,
+                   "Jaccard": L.ngt_set_property_distance_type_jaccard,
+                   "Cosine": L.ngt_set_property_distance_type_cosine,
+                   "Normalized Angle": L.ngt_set_property_distance_type_normalized_angle,
+                   "Normalized Cosine": L.ngt_set_property_distance_type_normalized_cosine}
+        ok = ok and setters[distance_type](prop, err)
+        index = L.ngt_create_graph_and_tree(path.encode(), prop, err) if ok else None
+        msg = _err_string(L, err)
+        if index:
+            L.ngt_close_index(index)
+        L.ngt_destroy_property(prop)
+        L.ngt_destroy_error_object(err)
+        if not ok or not index:
+            raise NativeError(msg)
+
+    def insert_object(self, obj):
+        """Append one object (ngt_insert_index_as_float); returns its id."""
+        o = np.ascontiguousarray(obj, dtype=np.float32)
+        oid = self._L.ngt_insert_index_as_float(self.index, o.ctypes.data_as(POINTER(c_float)), len(o), self.err)
+        if oid == 0:
+            raise NativeError(_err_string(self._L, self.err))
+        return oid
+
+    def insert(self, objects, num_threads=8):
+        """Append objects and build the index (python/ngt/base.py:378-389)."""
+        for o in objects:
+            self.insert_object(o)
+        self.build_index(num_threads)
+
+    def build_index(self, num_threads=8):
+        """ngt_create_index: ANNG + DVP tree of the appended objects, built on the GPU."""
+        self._check(self._L.ngt_create_index(self.index, num_threads, self.err), self.err)
+
     def search(self, query, k=20, epsilon=0.1, radius=-1.0):
         """k nearest neighbours of `query` (ngt_search_index, Capi.cpp:346-375).
         Returns a list of ObjectDistance (id, distance) ascending."""

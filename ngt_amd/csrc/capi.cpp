@@ -191,6 +191,67 @@ std::string append_object(CapiIndex* ix, const T* obj, uint32_t dim, uint32_t& i
   return "";
 }
 
+// GraphAndTreeIndex::createIndex for the objects appended since the last
+// build: ANNG with the tree, on the device; the host mirror receives the
+// graph (CSR + distances) and the DVP tree for ngt_save_index and searches.
+std::string build_anng(CapiIndex* ix) {
+  HostIndex& h = ix->host;
+  if (h.prop.edge_size_for_creation == 0) return "";  // createIndex returns at once (Index.cpp:1162-1164)
+  if (h.prop.graph_type != 1) return "index construction supports graphType ANNG only";
+  if (h.prop.index_type != 0) return "index construction supports GraphAndTree indexes only";
+  for (uint64_t v = 0; v < h.nrows && v + 1 < h.edge_off.size(); v++)
+    if (h.edge_off[v + 1] != h.edge_off[v])
+      return "incremental construction into an index that already has a graph is not implemented";
+  if (h.nrows < 2) return "";
+  std::string e = sync_device(ix);
+  if (!e.empty()) return e;
+  ngt_amd_build_params p{};
+  p.edge_size_for_creation = h.prop.edge_size_for_creation;
+  p.edge_size_for_search = h.prop.edge_size_for_search;
+  p.batch_size_for_creation = h.prop.batch_size_for_creation;
+  p.seed_size = h.prop.seed_size;
+  p.epsilon_for_creation = (float)h.prop.epsilon_for_creation;
+  if (ngt_amd_build_begin(ix->dev, &p) || ngt_amd_build_insert(ix->dev, 1, h.nrows)) return amd_err();
+  uint64_t gsize = 0, ne = 0;
+  if (ngt_amd_build_graph_size(ix->dev, &gsize, &ne)) return amd_err();
+  std::vector<uint64_t> off(gsize + 1);
+  h.edges.resize(ne);
+  h.edge_dists.resize(ne);
+  if (ngt_amd_build_get_graph(ix->dev, off.data(), h.edges.data(), h.edge_dists.data())) return amd_err();
+  h.edge_off.assign(h.nrows + 1, ne);
+  for (uint64_t v = 0; v <= h.nrows && v <= gsize; v++) h.edge_off[v] = off[v];
+  h.prevsize.assign(h.nrows, 0);
+  uint32_t nl = 0, ni = 0;
+  uint64_t nli = 0;
+  if (ngt_amd_build_tree_size(ix->dev, &nl, &ni, &nli)) return amd_err();
+  ngt_amd::HostTree& t = h.tree;
+  t = ngt_amd::HostTree();
+  t.leaf_parent.resize(nl);
+  t.leaf_off.resize((size_t)nl + 1);
+  t.leaf_ids.resize(nli);
+  t.leaf_dists.resize(nli);
+  t.leaf_has_pivot.resize(nl);
+  t.leaf_pivot.resize((size_t)nl * h.row_bytes);
+  t.in_parent.resize(ni);
+  t.in_pivot.resize((size_t)ni * h.row_bytes);
+  t.in_child.resize((size_t)ni * 5);
+  t.in_border.resize((size_t)ni * 4);
+  if (ngt_amd_build_get_tree(ix->dev, t.leaf_parent.data(), t.leaf_off.data(), t.leaf_ids.data(),
+                             t.leaf_dists.data(), t.leaf_has_pivot.data(), t.leaf_pivot.data(), t.in_parent.data(),
+                             t.in_pivot.data(), t.in_child.data(), t.in_border.data()))
+    return amd_err();
+  t.leaf_valid.assign(nl, 1);
+  t.leaf_valid[0] = 0;
+  t.in_valid.assign(ni, 1);
+  if (ni) t.in_valid[0] = 0;
+  for (uint32_t i = 1; i < nl; i++)  // LeafNode::serialize writes the pivot unless the leaf is an empty root
+    t.leaf_has_pivot[i] = !((t.leaf_parent[i] & 0x7fffffffu) == 0 && t.leaf_off[i + 1] == t.leaf_off[i]);
+  t.root = ni > 1 ? 1u : 0x80000001u;
+  t.present = nl > 1;
+  ix->device_stale = true;
+  return "";
+}
+
 const char* kNotImplemented =
     "not implemented in the MI355X build yet (index construction / graph maintenance, SURVEY.md 8(f))";
 
@@ -554,13 +615,24 @@ bool ngt_batch_insert_index(NGTIndex index, float* obj, uint32_t num_obj, uint32
   return ngt_create_index(index, 0, error);
 }
 bool ngt_create_index(NGTIndex index, uint32_t pool_size, NGTError error) {
+  // NGT::Index::createIndex(threadPoolSize) -> GraphAndTreeIndex::createIndex
+  // (Index.cpp:1158-1257), built on the device (ngt_amd_build_*, build.cpp).
+  // pool_size only sets the reference's host thread count: the result does
+  // not depend on it.
   (void)pool_size;
   if (index == NULL) {
     param_error(error, __FUNCTION__, "index = 0");
     return false;
   }
-  set_error(error, __FUNCTION__, kNotImplemented);
-  return false;
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  HostIndex& h = ix->host;
+  std::string e = build_anng(ix);
+  if (!e.empty()) {
+    set_error(error, __FUNCTION__, e);
+    return false;
+  }
+  (void)h;
+  return true;
 }
 bool ngt_remove_index(NGTIndex index, ObjectID id, NGTError error) {
   (void)id;

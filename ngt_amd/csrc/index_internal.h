@@ -82,6 +82,53 @@ struct SearchCtx {
   }
 };
 
+// glibc random(3) TYPE_3 (random_r), host side: the rand() stream of a fresh
+// process (srand(1)), for getRandomSeeds during construction.
+struct GlibcRandHost {
+  uint32_t s[31];
+  int f = 3, r = 0;
+  void seed(uint32_t sd) {
+    int32_t word = (int32_t)(sd == 0 ? 1u : sd);
+    s[0] = (uint32_t)word;
+    for (int i = 1; i < 31; i++) {
+      int32_t hi = word / 127773, lo = word % 127773;
+      word = 16807 * lo - 2836 * hi;
+      if (word < 0) word += 2147483647;
+      s[i] = (uint32_t)word;
+    }
+    f = 3;
+    r = 0;
+    for (int i = 0; i < 310; i++) next();
+  }
+  int next() {
+    s[f] += s[r];
+    int res = (int)((s[f] >> 1) & 0x7fffffff);
+    f = f == 30 ? 0 : f + 1;
+    r = r == 30 ? 0 : r + 1;
+    return res;
+  }
+};
+
+// ANNG construction state (build.cpp): the graph being built (host, sorted
+// edge lists), the DVP tree being built (HBM, fixed-capacity node arrays) and
+// the padded search adjacency the insertion searches read (HBM).
+struct BuildState {
+  int32_t edge_size_for_creation = 10, edge_size_for_search = 40, batch_size = 200, seed_size = 10;
+  float epsilon_for_creation = 0.1f;
+  std::vector<std::vector<std::pair<uint32_t, float>>> graph;  // graph repository, slot = object id
+  std::vector<uint8_t> in_graph;
+  uint64_t graph_size = 0;       // GraphRepository::size() (max inserted id + 1, 0 when empty)
+  // tree (leaf ids and internal ids start at 1; leaf 1 is the initial root)
+  DevBuf<uint32_t> lf_parent, lf_count, lf_ids, in_parent, in_child, counts;
+  DevBuf<uint8_t> lf_has_pivot, lf_pivot, in_pivot;
+  DevBuf<float> lf_dist, in_border;
+  uint32_t leaf_cap_nodes = 0, in_cap_nodes = 0;
+  uint32_t n_leaf = 2, n_internal = 1;  // next ids
+  uint32_t root = 0x80000001u;
+  GlibcRandHost rnd;
+  uint64_t adj_stride = 0;
+};
+
 }  // namespace ngt_amd
 
 struct ngt_amd_index {
@@ -123,8 +170,10 @@ struct ngt_amd_index {
   DevBuf<int> error;
   uint32_t spill_cap = 1u << 16;
   hipStream_t stream = nullptr;
+  ngt_amd::BuildState* build = nullptr;    // ANNG construction (build.cpp)
   ~ngt_amd_index() {
     for (auto* c : ctxs) delete c;
+    delete build;
   }
   int cu_count = 256;
   size_t lds_per_cu = 160 * 1024;

@@ -29,7 +29,9 @@ struct TreeSeedArgs {
   const float* in_border;        // [n_internal][children-1]
   uint32_t children;
   uint32_t root;                 // raw Node::ID of the root
-  const uint64_t* leaf_off;      // [n_leaf+1]
+  const uint64_t* leaf_off;      // [n_leaf+1] (CSR leaves), or
+  const uint32_t* leaf_count;    // [n_leaf] with leaf j's ids at leaf_ids + j * leaf_stride
+  uint32_t leaf_stride;
   const uint32_t* leaf_ids;
   uint32_t seed_size;            // property.seedSize (0 => k)
   uint32_t k;
@@ -103,6 +105,39 @@ struct MergeArgs {
   float* out_dists;
   uint32_t* out_n;               // [nq]
 };
+
+// ---- ANNG construction (build_kernels.hip) ----------------------------------
+struct TreeBuildArgs {
+  const uint8_t* rows;           // object rows (row_bytes apart)
+  uint64_t row_bytes;
+  int dp;
+  // leaves [leaf_cap_nodes]: parent (raw Node::ID), pivot row, objects (id, distance)
+  uint32_t* lf_parent;
+  uint8_t* lf_has_pivot;
+  uint8_t* lf_pivot;             // [L][row_bytes]
+  uint32_t* lf_count;
+  uint32_t* lf_ids;              // [L][leaf_cap]
+  float* lf_dist;                // [L][leaf_cap]
+  uint32_t leaf_cap;             // >= leaf_size + 1
+  // internal nodes [in_cap_nodes]
+  uint32_t* in_parent;
+  uint8_t* in_pivot;             // [I][row_bytes]
+  uint32_t* in_child;            // [I][5]
+  float* in_border;              // [I][4]
+  uint32_t* counts;              // [0] next leaf id, [1] next internal id, [2] root raw id
+  uint32_t leaf_cap_nodes, in_cap_nodes;
+  uint32_t leaf_size;            // leafObjectsSize (100)
+  const uint32_t* ids;           // batch object ids, batch order
+  const uint8_t* insert_flag;    // [n] 0 = not inserted into the tree
+  uint32_t n;
+  int* error;
+};
+
+hipError_t launch_tree_insert(const TreeBuildArgs& a, int metric, int otype, hipStream_t s);
+hipError_t launch_adj_scatter(uint32_t* adj, uint64_t stride, const uint32_t* nodes, const uint32_t* vals,
+                              uint32_t n, hipStream_t s);
+hipError_t launch_gather_rows(uint8_t* dst, const uint8_t* rows, uint64_t row_bytes, const uint32_t* ids,
+                              uint32_t n, hipStream_t s);
 
 hipError_t launch_distances(const DistanceArgs& a, int metric, int otype, hipStream_t s);
 hipError_t launch_merge_results(const MergeArgs& a, hipStream_t s);

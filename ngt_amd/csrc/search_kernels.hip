@@ -106,8 +106,9 @@ __global__ void __launch_bounds__(64) ngt_tree_seed_kernel(TreeSeedArgs a) {
       node = a.in_child[(uint64_t)iid * a.children + mid];
     }
     const uint32_t lid = node & 0x7fffffffu;
-    const uint64_t b = a.leaf_off[lid], e = a.leaf_off[lid + 1];
-    uint32_t n = (uint32_t)(e - b);
+    // leaves as CSR (a loaded index) or fixed-stride rows (the tree under construction)
+    const uint64_t b = a.leaf_count ? (uint64_t)lid * a.leaf_stride : a.leaf_off[lid];
+    uint32_t n = a.leaf_count ? a.leaf_count[lid] : (uint32_t)(a.leaf_off[lid + 1] - b);
     uint32_t* out = a.seeds + (uint64_t)qi * a.seed_stride;
     if (n > a.seed_stride) n = a.seed_stride;
     for (uint32_t i = lane; i < n; i += 64) out[i] = a.leaf_ids[b + i];

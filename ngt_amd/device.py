@@ -160,6 +160,43 @@ class DeviceIndex(object):
                                       len(oid), out.ctypes.data))
         return out
 
+    # ---- ANNG construction (GraphAndTreeIndex::createIndex) -----------------
+    def build_anng(self, first_id=1, end_id=None, edge_size_for_creation=10, edge_size_for_search=40,
+                   batch_size_for_creation=200, seed_size=10, epsilon_for_creation=0.1, begin=True):
+        """Build the ANNG + DVP tree of the objects on the device; returns
+        (offsets, ids, dists) of the graph and the tree dict (read_tre layout)."""
+        from ._sigs import BuildParams
+        if begin:
+            prm = BuildParams(edge_size_for_creation, edge_size_for_search, batch_size_for_creation, seed_size,
+                              epsilon_for_creation, 0)
+            _chk(self.L.ngt_amd_build_begin(self.h, byref(prm)))
+        _chk(self.L.ngt_amd_build_insert(self.h, first_id, self.nrows if end_id is None else end_id))
+        return self.build_graph(), self.build_tree()
+
+    def build_graph(self):
+        gs, ne = ctypes.c_uint64(), ctypes.c_uint64()
+        _chk(self.L.ngt_amd_build_graph_size(self.h, byref(gs), byref(ne)))
+        offs = np.zeros(gs.value + 1, np.uint64)
+        ids = np.zeros(max(ne.value, 1), np.uint32)
+        ds = np.zeros(max(ne.value, 1), np.float32)
+        _chk(self.L.ngt_amd_build_get_graph(self.h, offs.ctypes.data, ids.ctypes.data, ds.ctypes.data))
+        return offs, ids[:ne.value], ds[:ne.value]
+
+    def build_tree(self):
+        nl, ni, nli = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+        _chk(self.L.ngt_amd_build_tree_size(self.h, byref(nl), byref(ni), byref(nli)))
+        nl, ni, nli = nl.value, ni.value, nli.value
+        t = {"leaf_parent": np.zeros(nl, np.uint32), "leaf_off": np.zeros(nl + 1, np.uint64),
+             "leaf_ids": np.zeros(max(nli, 1), np.uint32), "leaf_dists": np.zeros(max(nli, 1), np.float32),
+             "leaf_has_pivot": np.zeros(nl, np.uint8), "leaf_pivot": np.zeros((nl, self.dp), self.dtype),
+             "in_parent": np.zeros(ni, np.uint32), "in_pivot": np.zeros((ni, self.dp), self.dtype),
+             "in_child": np.zeros((ni, 5), np.uint32), "in_border": np.zeros((ni, 4), np.float32)}
+        _chk(self.L.ngt_amd_build_get_tree(self.h, *[t[k].ctypes.data for k in (
+            "leaf_parent", "leaf_off", "leaf_ids", "leaf_dists", "leaf_has_pivot", "leaf_pivot", "in_parent",
+            "in_pivot", "in_child", "in_border")]))
+        t["leaf_ids"], t["leaf_dists"] = t["leaf_ids"][:nli], t["leaf_dists"][:nli]
+        return t
+
     # ---- NGTQG quantized graph (L2 float) ---------------------------------
     def qg_set_quantizer(self, global_centroid, local):
         """global_centroid: [dim]; local: [M, 16, dsub] (local ids 1..16)."""
