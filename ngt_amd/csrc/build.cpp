@@ -23,10 +23,12 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "../../include/ngt_amd.h"
@@ -151,6 +153,17 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   HIP_OK(d_flag.alloc(B));
   std::vector<uint32_t> h_tseeds((size_t)B * SS), h_tcnt(B), h_oi((size_t)B * K), h_on(B);
   std::vector<float> h_od((size_t)B * K);
+  // NGT_AMD_BUILD_PROFILE=1: per-stage wall time (stream synchronised at each mark)
+  const bool prof = getenv("NGT_AMD_BUILD_PROFILE") != nullptr;
+  double st[6] = {0, 0, 0, 0, 0, 0};
+  auto t_last = std::chrono::steady_clock::now();
+  auto mark = [&](int i) {
+    if (!prof) return;
+    (void)hipStreamSynchronize(s);
+    auto t = std::chrono::steady_clock::now();
+    st[i] += std::chrono::duration<double>(t - t_last).count();
+    t_last = t;
+  };
 
   for (size_t pos = 0; pos < todo.size(); pos += B) {
     const uint32_t n = (uint32_t)std::min<size_t>(B, todo.size() - pos);
@@ -184,6 +197,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     HIP_OK(hipMemcpyAsync(h_tseeds.data(), d_tseeds.p, (size_t)n * SS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(h_tcnt.data(), d_tcnt.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
+    mark(0);
     std::vector<uint32_t> seeds;
     std::vector<uint64_t> soff(n + 1, 0);
     for (uint32_t i = 0; i < n; i++) {
@@ -226,6 +240,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
       HIP_OK(hipMemcpyAsync(h_od.data(), d_od.p, (size_t)n * K * sizeof(float), hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(h_on.data(), d_on.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
+    mark(1);
 
     // ---- 3. pairwise distances inside the batch (Index.cpp:690-703) --------
     const uint64_t npairs = (uint64_t)n * (n - 1) / 2;
@@ -258,6 +273,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     if (herr) return fail("ngt_amd_build_insert: device error flag %d in the insertion search", herr);
+    mark(2);
 
     // ---- merge, sort, cut; insertANNGNode ----------------------------------
     std::vector<uint32_t> dirty;
@@ -287,6 +303,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
       flag[i] = (objs.empty() || objs[0].second != 0.0f) ? 1 : 0;
     }
 
+    mark(3);
     // ---- 4. DVPTree::insert of the batch ----------------------------------
     HIP_OK(hipMemcpyAsync(d_flag.p, flag.data(), n, hipMemcpyHostToDevice, s));
     TreeBuildArgs ta{};
@@ -313,6 +330,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     ta.n = n;
     ta.error = ix->error.p;
     HIP_OK(launch_tree_insert(ta, ix->metric, ix->otype, s));
+    mark(4);
 
     // ---- refresh the padded adjacency of the touched nodes -----------------
     std::sort(dirty.begin(), dirty.end());
@@ -338,7 +356,11 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     b.n_leaf = hc[0];
     b.n_internal = hc[1];
     b.root = hc[2];
+    mark(5);
   }
+  if (prof)
+    fprintf(stderr, "build_insert %zu objects: seeds %.3f s, search %.3f s, pair distances %.3f s, host graph %.3f s, "
+            "tree insert %.3f s, adjacency %.3f s\n", todo.size(), st[0], st[1], st[2], st[3], st[4], st[5]);
   return 0;
 }
 

@@ -195,6 +195,8 @@ class DeviceIndex(object):
             "leaf_parent", "leaf_off", "leaf_ids", "leaf_dists", "leaf_has_pivot", "leaf_pivot", "in_parent",
             "in_pivot", "in_child", "in_border")]))
         t["leaf_ids"], t["leaf_dists"] = t["leaf_ids"][:nli], t["leaf_dists"][:nli]
+        # DVPTree::getRootNode (lib/NGT/Tree.h:219-235): internal 1 once the root leaf has split
+        t["root"] = 1 if ni > 1 else 0x80000001
         return t
 
     # ---- NGTQG quantized graph (L2 float) ---------------------------------
