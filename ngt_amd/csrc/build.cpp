@@ -157,6 +157,14 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   const bool prof = getenv("NGT_AMD_BUILD_PROFILE") != nullptr;
   double st[6] = {0, 0, 0, 0, 0, 0};
   auto t_last = std::chrono::steady_clock::now();
+  DevBuf<uint64_t> d_cnt;
+  std::vector<uint64_t> h_cnt;
+  double k_ms = 0, dc = 0, ex = 0, ex_max = 0;
+  uint64_t nsearched = 0;
+  if (prof) {
+    HIP_OK(d_cnt.alloc((size_t)B * NGT_AMD_COUNTERS_PER_QUERY));
+    h_cnt.resize((size_t)B * NGT_AMD_COUNTERS_PER_QUERY);
+  }
   auto mark = [&](int i) {
     if (!prof) return;
     (void)hipStreamSynchronize(s);
@@ -234,8 +242,23 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
       p.edge_size = -1;  // sc.edgeSize default -> edgeSizeForSearch
       p.seed_mode = NGT_AMD_SEED_GIVEN;
       p.visited_hash_log2 = 0;
-      if (ngt_amd_search_device(ix, &p, d_q.p, rb, n, d_seeds.p, d_soff.p, d_oi.p, d_od.p, d_on.p, nullptr, s))
+      if (ngt_amd_search_device(ix, &p, d_q.p, rb, n, d_seeds.p, d_soff.p, d_oi.p, d_od.p, d_on.p,
+                                prof ? d_cnt.p : nullptr, s))
         return -1;
+      if (prof) {
+        HIP_OK(hipMemcpyAsync(h_cnt.data(), d_cnt.p, (size_t)n * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
+                              hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        k_ms += ngt_amd_last_search_kernel_ms(ix);
+        uint64_t mx = 0;
+        for (uint32_t i = 0; i < n; i++) {
+          dc += (double)h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY];
+          ex += (double)h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + 2];
+          mx = std::max(mx, h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + 2]);
+        }
+        ex_max += (double)mx;
+        nsearched += n;
+      }
       HIP_OK(hipMemcpyAsync(h_oi.data(), d_oi.p, (size_t)n * K * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(h_od.data(), d_od.p, (size_t)n * K * sizeof(float), hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(h_on.data(), d_on.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -360,7 +383,10 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   }
   if (prof)
     fprintf(stderr, "build_insert %zu objects: seeds %.3f s, search %.3f s, pair distances %.3f s, host graph %.3f s, "
-            "tree insert %.3f s, adjacency %.3f s\n", todo.size(), st[0], st[1], st[2], st[3], st[4], st[5]);
+            "tree insert %.3f s, adjacency %.3f s; search kernel %.3f s, per query %.1f distances %.1f expansions, "
+            "mean per-batch max expansions %.1f\n", todo.size(), st[0], st[1], st[2], st[3], st[4], st[5], k_ms / 1e3,
+            dc / std::max<uint64_t>(nsearched, 1), ex / std::max<uint64_t>(nsearched, 1),
+            ex_max / std::max<double>(1.0, (double)((todo.size() + B - 1) / B)));
   return 0;
 }
 
