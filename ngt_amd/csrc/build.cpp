@@ -138,8 +138,15 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     if (ix->h_valid[id] && !b.in_graph[id]) todo.push_back((uint32_t)id);
 
   const uint32_t B = (uint32_t)b.batch_size, K = (uint32_t)b.edge_size_for_creation;
+  struct Ev {
+    hipEvent_t e = nullptr;
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev_copy;
+  HIP_OK(hipEventCreateWithFlags(&ev_copy.e, hipEventDisableTiming));
   const uint32_t SS = kTreeSeedStride;
-  DevBuf<uint32_t> d_ids, d_tseeds, d_tcnt, d_seeds, d_oi, d_on, d_pq, d_po, d_dirty, d_vals;
+  DevBuf<uint32_t> d_ids, d_tseeds, d_tcnt, d_seeds, d_oi, d_on, d_dirty, d_vals;
   DevBuf<uint64_t> d_soff;
   DevBuf<float> d_od, d_pd;
   DevBuf<uint8_t> d_q, d_flag;
@@ -151,15 +158,25 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   HIP_OK(d_od.alloc((size_t)B * K));
   HIP_OK(d_on.alloc(B));
   HIP_OK(d_flag.alloc(B));
-  std::vector<uint32_t> h_tseeds((size_t)B * SS), h_tcnt(B), h_oi((size_t)B * K), h_on(B);
-  std::vector<float> h_od((size_t)B * K);
+  DevBuf<uint32_t> d_pleaf, d_pcnt;
+  DevBuf<float> d_pdist;
+  HIP_OK(d_pleaf.alloc(B));
+  HIP_OK(d_pcnt.alloc(B));
+  HIP_OK(d_pdist.alloc(B));
+  DevBuf<uint32_t> d_mi, d_mn;
+  DevBuf<float> d_md;
+  HIP_OK(d_mi.alloc((size_t)B * K));
+  HIP_OK(d_md.alloc((size_t)B * K));
+  HIP_OK(d_mn.alloc(B));
+  std::vector<uint32_t> h_tseeds((size_t)B * SS), h_tcnt(B), h_mi((size_t)B * K), h_mn(B);
+  std::vector<float> h_md((size_t)B * K);
   // NGT_AMD_BUILD_PROFILE=1: per-stage wall time (stream synchronised at each mark)
   const bool prof = getenv("NGT_AMD_BUILD_PROFILE") != nullptr;
   double st[6] = {0, 0, 0, 0, 0, 0};
   auto t_last = std::chrono::steady_clock::now();
   DevBuf<uint64_t> d_cnt;
   std::vector<uint64_t> h_cnt;
-  double k_ms = 0, dc = 0, ex = 0, ex_max = 0;
+  double k_ms = 0, dc = 0, ex = 0, ex_max = 0, c3 = 0, c5 = 0, c6 = 0, c7 = 0, c5_max = 0;
   uint64_t nsearched = 0;
   if (prof) {
     HIP_OK(d_cnt.alloc((size_t)B * NGT_AMD_COUNTERS_PER_QUERY));
@@ -201,6 +218,11 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     t.seeds = d_tseeds.p;
     t.seed_stride = SS;
     t.seed_count = d_tcnt.p;
+    // the same descent locates each object's leaf for step 4
+    t.out_leaf = d_pleaf.p;
+    t.out_count = d_pcnt.p;
+    t.out_pdist = d_pdist.p;
+    t.leaf_pivot = b.lf_pivot.p;
     HIP_OK(launch_tree_seeds(t, ix->metric, ix->otype, s));
     HIP_OK(hipMemcpyAsync(h_tseeds.data(), d_tseeds.p, (size_t)n * SS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(h_tcnt.data(), d_tcnt.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -231,7 +253,6 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     }
 
     // ---- 2. insertion searches (searchForNNGInsertion, Index.h:1457-1479) --
-    std::fill(h_on.begin(), h_on.begin() + n, 0u);
     if (!seeds.empty()) {
       HIP_OK(d_seeds.upload(seeds.data(), seeds.size()));
       HIP_OK(d_soff.upload(soff.data(), n + 1));
@@ -255,80 +276,50 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
           dc += (double)h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY];
           ex += (double)h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + 2];
           mx = std::max(mx, h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + 2]);
+          const uint64_t* c = h_cnt.data() + (size_t)i * NGT_AMD_COUNTERS_PER_QUERY;
+          c3 += (double)c[3];
+          c5 += (double)c[5];
+          c6 += (double)c[6];
+          c7 += (double)c[7];
+          c5_max = std::max(c5_max, (double)c[5]);
         }
         ex_max += (double)mx;
         nsearched += n;
       }
-      HIP_OK(hipMemcpyAsync(h_oi.data(), d_oi.p, (size_t)n * K * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      HIP_OK(hipMemcpyAsync(h_od.data(), d_od.p, (size_t)n * K * sizeof(float), hipMemcpyDeviceToHost, s));
-      HIP_OK(hipMemcpyAsync(h_on.data(), d_on.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    } else {
+      HIP_OK(hipMemsetAsync(d_on.p, 0, n * sizeof(uint32_t), s));
     }
     mark(1);
 
-    // ---- 3. pairwise distances inside the batch (Index.cpp:690-703) --------
+    // ---- 3. pairwise distances inside the batch (Index.cpp:690-703), then the
+    //         merge / sort / cut of insertMultipleSearchResults (:673-727) -------
     const uint64_t npairs = (uint64_t)n * (n - 1) / 2;
-    std::vector<float> h_pd(npairs);
-    if (npairs) {
-      std::vector<uint32_t> pq(npairs), po(npairs);
-      uint64_t k = 0;
-      for (uint32_t i = 0; i < n; i++)
-        for (uint32_t j = 0; j < i; j++, k++) {
-          pq[k] = i;       // comparator(*output[idxi].object, *output[idxj].object)
-          po[k] = ids[j];
-        }
-      HIP_OK(d_pq.upload(pq.data(), npairs));
-      HIP_OK(d_po.upload(po.data(), npairs));
-      HIP_OK(d_pd.alloc(npairs));
-      DistanceArgs da{};
-      da.rows = ix->rows.p;
-      da.row_bytes = rb;
-      da.queries = d_q.p;
-      da.query_bytes = rb;
-      da.qidx = d_pq.p;
-      da.oid = d_po.p;
-      da.out = d_pd.p;
-      da.npairs = npairs;
-      da.dp = (int)ix->dp;
-      HIP_OK(launch_distances(da, ix->metric, ix->otype, s));
-      HIP_OK(hipMemcpyAsync(h_pd.data(), d_pd.p, npairs * sizeof(float), hipMemcpyDeviceToHost, s));
-    }
-    int herr = 0;
-    HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    if (herr) return fail("ngt_amd_build_insert: device error flag %d in the insertion search", herr);
+    if (npairs) HIP_OK(d_pd.alloc(npairs));
+    BatchPairArgs bp{};
+    bp.rows = ix->rows.p;
+    bp.row_bytes = rb;
+    bp.dp = (int)ix->dp;
+    bp.batch = d_q.p;
+    bp.ids = d_ids.p;
+    bp.n = n;
+    bp.out = d_pd.p;
+    HIP_OK(launch_batch_pairs(bp, ix->metric, ix->otype, s));
+    BatchMergeArgs bm{};
+    bm.res_ids = d_oi.p;
+    bm.res_dists = d_od.p;
+    bm.res_n = d_on.p;
+    bm.K = K;
+    bm.ids = d_ids.p;
+    bm.pair = d_pd.p;
+    bm.n = n;
+    bm.out_ids = d_mi.p;
+    bm.out_dists = d_md.p;
+    bm.out_n = d_mn.p;
+    bm.flag = d_flag.p;
+    HIP_OK(launch_batch_merge(bm, s));
     mark(2);
 
-    // ---- merge, sort, cut; insertANNGNode ----------------------------------
-    std::vector<uint32_t> dirty;
-    std::vector<uint8_t> flag(n);
-    uint64_t pk = 0;
-    for (uint32_t i = 0; i < n; i++) {
-      std::vector<std::pair<uint32_t, float>> objs;
-      for (uint32_t j = 0; j < h_on[i]; j++) objs.push_back({h_oi[(size_t)i * K + j], h_od[(size_t)i * K + j]});
-      for (uint32_t j = 0; j < i; j++, pk++) objs.push_back({ids[j], h_pd[pk]});
-      std::sort(objs.begin(), objs.end(), od_less);
-      if (objs.size() > K) objs.resize(K);
-      const uint32_t id = ids[i];
-      // GraphRepository::insert(id, results) then addEdge(r.id, id, r.distance)
-      b.graph[id] = objs;
-      b.in_graph[id] = 1;
-      b.graph_size = std::max<uint64_t>(b.graph_size, (uint64_t)id + 1);
-      dirty.push_back(id);
-      for (const auto& r : objs) {
-        auto& node = b.graph[r.first];
-        const std::pair<uint32_t, float> e{id, r.second};
-        auto it = std::lower_bound(node.begin(), node.end(), e, od_less);
-        if (it != node.end() && it->first == id) return fail("NGT::addEdge: already existed! %u:%u", it->first, id);
-        if ((uint64_t)(it - node.begin()) < b.adj_stride) dirty.push_back(r.first);
-        node.insert(it, e);
-      }
-      // DVPTree insertion unless the object duplicates its nearest neighbour (Index.cpp:1201-1203)
-      flag[i] = (objs.empty() || objs[0].second != 0.0f) ? 1 : 0;
-    }
-
-    mark(3);
-    // ---- 4. DVPTree::insert of the batch ----------------------------------
-    HIP_OK(hipMemcpyAsync(d_flag.p, flag.data(), n, hipMemcpyHostToDevice, s));
+    // ---- 4. DVPTree::insert of the batch (device, overlaps the host graph work)
     TreeBuildArgs ta{};
     ta.rows = ix->rows.p;
     ta.row_bytes = rb;
@@ -350,10 +341,40 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     ta.leaf_size = 100;  // LeafNode::LeafObjectsSizeMax (Node.h:618)
     ta.ids = d_ids.p;
     ta.insert_flag = d_flag.p;
+    ta.pre_leaf = d_pleaf.p;
+    ta.pre_count = d_pcnt.p;
+    ta.pre_dist = d_pdist.p;
     ta.n = n;
     ta.error = ix->error.p;
+    // the merged lists go to the host while the tree insertion runs
+    HIP_OK(hipMemcpyAsync(h_mi.data(), d_mi.p, (size_t)n * K * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(h_md.data(), d_md.p, (size_t)n * K * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(h_mn.data(), d_mn.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(ev_copy.e, s));
     HIP_OK(launch_tree_insert(ta, ix->metric, ix->otype, s));
     mark(4);
+    HIP_OK(hipEventSynchronize(ev_copy.e));
+
+    // ---- insertANNGNode (Graph.h:611-625): the node, then the reverse edges --
+    std::vector<uint32_t> dirty;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t id = ids[i];
+      auto& objs = b.graph[id];
+      objs.resize(h_mn[i]);
+      for (uint32_t j = 0; j < h_mn[i]; j++) objs[j] = {h_mi[(size_t)i * K + j], h_md[(size_t)i * K + j]};
+      b.in_graph[id] = 1;
+      b.graph_size = std::max<uint64_t>(b.graph_size, (uint64_t)id + 1);
+      dirty.push_back(id);
+      for (const auto& r : objs) {
+        auto& node = b.graph[r.first];
+        const std::pair<uint32_t, float> e{id, r.second};
+        auto it = std::lower_bound(node.begin(), node.end(), e, od_less);
+        if (it != node.end() && it->first == id) return fail("NGT::addEdge: already existed! %u:%u", it->first, id);
+        if ((uint64_t)(it - node.begin()) < b.adj_stride) dirty.push_back(r.first);
+        node.insert(it, e);
+      }
+    }
+    mark(3);
 
     // ---- refresh the padded adjacency of the touched nodes -----------------
     std::sort(dirty.begin(), dirty.end());
@@ -368,13 +389,14 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     HIP_OK(d_vals.upload(vals.data(), vals.size()));
     HIP_OK(launch_adj_scatter(ix->adj.p, b.adj_stride, d_dirty.p, d_vals.p, (uint32_t)dirty.size(), s));
     uint32_t hc[3];
+    int herr = 0;
     HIP_OK(hipMemcpyAsync(hc, b.counts.p, sizeof hc, hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     if (herr) {
       (void)hipMemset(ix->error.p, 0, sizeof(int));
-      return fail("ngt_amd_build_insert: DVP tree insertion failed (device flag %d: 2 already existed, "
-                  "8 all split distances equal, 16 node capacity, 32 illegal pivot)", herr);
+      return fail("ngt_amd_build_insert: device error flag %d (1 unchecked-set spill full; DVP tree: 2 already "
+                  "existed, 8 all split distances equal, 16 node capacity, 32 illegal pivot)", herr);
     }
     b.n_leaf = hc[0];
     b.n_internal = hc[1];
@@ -382,11 +404,18 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     mark(5);
   }
   if (prof)
-    fprintf(stderr, "build_insert %zu objects: seeds %.3f s, search %.3f s, pair distances %.3f s, host graph %.3f s, "
+    fprintf(stderr, "build_insert %zu objects: seeds %.3f s, search %.3f s, pairs+merge %.3f s, host graph %.3f s, "
             "tree insert %.3f s, adjacency %.3f s; search kernel %.3f s, per query %.1f distances %.1f expansions, "
             "mean per-batch max expansions %.1f\n", todo.size(), st[0], st[1], st[2], st[3], st[4], st[5], k_ms / 1e3,
             dc / std::max<uint64_t>(nsearched, 1), ex / std::max<uint64_t>(nsearched, 1),
             ex_max / std::max<double>(1.0, (double)((todo.size() + B - 1) / B)));
+  if (prof) {
+    const double nq = (double)std::max<uint64_t>(nsearched, 1);
+    // counters [3], [5..7]: spilled-visited flag, max unchecked, 0, 0 -- or, in
+    // the NGT_AMD_STAMPS build, rest/pop/adjacency/eval cycles
+    fprintf(stderr, "build_insert counters per query: c3 %.4g c5 %.4g (max %.4g) c6 %.4g c7 %.4g\n", c3 / nq,
+            c5 / nq, c5_max, c6 / nq, c7 / nq);
+  }
   return 0;
 }
 

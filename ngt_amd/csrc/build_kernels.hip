@@ -207,6 +207,9 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
   SortItem* items = reinterpret_cast<SortItem*>(fs_cl + 128);
   double* var = reinterpret_cast<double*>(items + 128);
   float* D = reinterpret_cast<float*>(var + 128);  // [NF][NF]
+  uint32_t* repl_leaf = reinterpret_cast<uint32_t*>(D + (size_t)(LS + 1) * (LS + 1));  // [256]
+  uint32_t* repl_in = repl_leaf + 256;                                         // [256]
+  uint32_t nrepl = 0;
   const uint64_t rb = a.row_bytes;
   auto row = [&](uint32_t id) { return a.rows + (uint64_t)id * rb; };
 
@@ -215,7 +218,33 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
     const uint32_t id = a.ids[t];
     const uint8_t* q = row(id);
     // ---- leaf descent (DVPTree::search, SearchLeaf, radius 0) -------------
+    // Pre-located: the leaf found against the tree at batch start is still
+    // on the object's path unless a split of this batch replaced it, and a
+    // split replaces a leaf in place by an internal node whose subtree then
+    // holds the path -- descend from the first such node.  A leaf that was
+    // not empty at batch start keeps its pivot until it splits, so its
+    // pivot distance is the pre-computed one.
     uint32_t node = a.counts[2];
+    bool have_pd = false;
+    float pre_pd = 0.f;
+    if (a.pre_leaf) {
+      const uint32_t pl = a.pre_leaf[t];
+      node = kLeaf | pl;
+      uint32_t hit = 0xffffffffu;
+      for (uint32_t r0 = 0; r0 < nrepl; r0 += 64) {
+        const uint64_t m = ballot64(r0 + lane < nrepl && repl_leaf[r0 + lane] == pl);
+        if (m) {
+          hit = repl_in[r0 + __ffsll((long long)m) - 1];
+          break;
+        }
+      }
+      if (hit != 0xffffffffu) {
+        node = hit;
+      } else if (a.pre_count[t] != 0) {
+        have_pd = true;
+        pre_pd = a.pre_dist[t];
+      }
+    }
     while (!(node & kLeaf)) {
       const uint32_t iid = node;
       const float d = dist1<M, T>(q, a.in_pivot + (uint64_t)iid * rb, a.dp);
@@ -231,8 +260,10 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
     const uint32_t cnt = a.lf_count[lid];
     // ---- DVPTree::insert(iobj, leaf): duplicate check (Tree.cpp:48-87) -----
     bool skip = false;
+    float pd = pre_pd;
+    if (cnt != 0 && !have_pd) pd = dist1<M, T>(q, a.lf_pivot + (uint64_t)lid * rb, a.dp);
     if (cnt != 0) {
-      const float d = dist1<M, T>(q, a.lf_pivot + (uint64_t)lid * rb, a.dp);
+      const float d = pd;
       for (uint32_t base = 0; base < cnt && !skip; base += 64) {
         uint64_t eq = ballot64(base + lane < cnt && ldst[base + lane] == d);
         while (eq) {
@@ -260,7 +291,7 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
           a.lf_count[lid] = 1;
         }
       } else {
-        const float d = dist1<M, T>(q, a.lf_pivot + (uint64_t)lid * rb, a.dp);
+        const float d = pd;
         if (lane == 0) {
           lids[cnt] = id;
           ldst[cnt] = d;
@@ -394,6 +425,18 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
       return;
     }
     uint32_t ln[5] = {lid, nl0, nl0 + 1, nl0 + 2, nl0 + 3};
+    {
+      bool known = false;
+      for (uint32_t r0 = 0; r0 < nrepl; r0 += 64)
+        known |= ballot64(r0 + lane < nrepl && repl_leaf[r0 + lane] == lid) != 0;
+      if (!known && nrepl < 256) {
+        if (lane == 0) {
+          repl_leaf[nrepl] = lid;
+          repl_in[nrepl] = inid;
+        }
+        nrepl++;
+      }
+    }
     if (lane == 0) {
       for (int c = 0; c < 5; c++) {
         a.lf_count[ln[c]] = 0;
@@ -464,6 +507,64 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
   }
 }
 
+// Pair distances of a creation batch: comparator(object i, object j), j < i
+// (Index.cpp:690-703), one quad per pair, stored in the order the reference
+// visits them.
+template <int M, typename T>
+__global__ void __launch_bounds__(256) ngt_batch_pairs_kernel(BatchPairArgs a) {
+  const int g = threadIdx.x & 3;
+  const uint64_t quad = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+  const uint64_t np = (uint64_t)a.n * (a.n - 1) / 2;
+  for (uint64_t p = quad; p < np; p += nquads) {
+    // p = i(i-1)/2 + j: i from the closed form, corrected for rounding
+    uint64_t i = (uint64_t)((1.0 + sqrt(1.0 + 8.0 * (double)p)) * 0.5);
+    while (i * (i - 1) / 2 > p) i--;
+    while ((i + 1) * i / 2 <= p) i++;
+    const uint64_t j = p - i * (i - 1) / 2;
+    const T* q = reinterpret_cast<const T*>(a.batch + i * a.row_bytes);
+    const T* x = row_ptr<T>(a.rows, a.row_bytes, a.ids[j]);
+    const float d = quad_distance<M, T>(q, x, a.dp, g);
+    if (g == 0) a.out[p] = d;
+  }
+}
+
+// One wave per batch object i: the K smallest (distance, id) keys among its
+// search results and the pairs (i, j < i) -- std::sort + resize on a total
+// order, so K rounds of "smallest key above the previous one" select the
+// same list.
+__global__ void __launch_bounds__(64) ngt_batch_merge_kernel(BatchMergeArgs a) {
+  const int lane = lane_id();
+  for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const uint32_t nr = a.res_n[i];
+    const uint32_t c = nr + i;
+    const uint64_t pb = (uint64_t)i * (i - 1) / 2;
+    const uint32_t want = c < a.K ? c : a.K;
+    uint64_t prev = 0, first = 0;
+    for (uint32_t r = 0; r < want; r++) {
+      uint64_t best = ~0ull;
+      for (uint32_t t = lane; t < c; t += 64) {
+        uint64_t key;
+        if (t < nr) key = make_key(a.res_dists[(uint64_t)i * a.K + t], a.res_ids[(uint64_t)i * a.K + t]);
+        else key = make_key(a.pair[pb + (t - nr)], a.ids[t - nr]);
+        if ((r == 0 || key > prev) && key < best) best = key;
+      }
+      best = wave_min_u64(best);
+      if (lane == 0) {
+        a.out_ids[(uint64_t)i * a.K + r] = key_id(best);
+        a.out_dists[(uint64_t)i * a.K + r] = key_dist(best);
+      }
+      if (r == 0) first = best;
+      prev = best;
+    }
+    if (lane == 0) {
+      a.out_n[i] = want;
+      // the tree gets the object unless it duplicates its nearest neighbour
+      a.flag[i] = (want == 0 || key_dist(first) != 0.0f) ? 1 : 0;
+    }
+  }
+}
+
 // Rows `nodes[i]` of the padded adjacency <- vals[i][0..stride).
 __global__ void __launch_bounds__(256) ngt_adj_scatter_kernel(uint32_t* adj, uint64_t stride,
                                                               const uint32_t* nodes, const uint32_t* vals,
@@ -529,11 +630,28 @@ hipError_t launch_tree_insert(const TreeBuildArgs& a, int metric, int otype, hip
   if (a.n == 0) return hipSuccess;
   const uint32_t nf = a.leaf_size + 1;
   const size_t lds = 128 * (4 + 4 + 4 + 4) + 128 * sizeof(SortItem) + 128 * sizeof(double) +
-                     (size_t)nf * nf * sizeof(float);
+                     (size_t)nf * nf * sizeof(float) + 2 * 256 * sizeof(uint32_t);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
 #define L_TI(MM, TT) hipLaunchKernelGGL((ngt_tree_insert_kernel<MM, TT>), dim3(1), dim3(64), lds, s, a)
   NGT_BUILD_DISPATCH(metric, otype, L_TI);
 #undef L_TI
+  return hipGetLastError();
+}
+
+hipError_t launch_batch_pairs(const BatchPairArgs& a, int metric, int otype, hipStream_t s) {
+  if (a.n < 2) return hipSuccess;
+  const uint64_t np = (uint64_t)a.n * (a.n - 1) / 2;
+  uint64_t blocks = (np * 4 + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+#define L_BP(MM, TT) hipLaunchKernelGGL((ngt_batch_pairs_kernel<MM, TT>), dim3((uint32_t)blocks), dim3(256), 0, s, a)
+  NGT_BUILD_DISPATCH(metric, otype, L_BP);
+#undef L_BP
+  return hipGetLastError();
+}
+
+hipError_t launch_batch_merge(const BatchMergeArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ngt_batch_merge_kernel, dim3(a.n < 4096 ? a.n : 4096), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

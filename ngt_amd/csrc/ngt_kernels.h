@@ -40,6 +40,12 @@ struct TreeSeedArgs {
   uint32_t seed_stride;
   uint32_t* seed_count;          // [nq]
   uint32_t* tree_ndist;          // [nq] or null
+  // construction only (all null otherwise): the leaf each query descends to,
+  // its object count, and the distance to its pivot when the count is > 0
+  uint32_t* out_leaf;            // [nq]
+  uint32_t* out_count;           // [nq]
+  float* out_pdist;              // [nq]
+  const uint8_t* leaf_pivot;     // [n_leaf][row_bytes]
 };
 
 struct SearchArgs {
@@ -129,10 +135,44 @@ struct TreeBuildArgs {
   uint32_t leaf_size;            // leafObjectsSize (100)
   const uint32_t* ids;           // batch object ids, batch order
   const uint8_t* insert_flag;    // [n] 0 = not inserted into the tree
+  // leaf / count / pivot distance of each batch object against the tree at
+  // batch start (TreeSeedArgs::out_*), or null to descend from the root
+  const uint32_t* pre_leaf;
+  const uint32_t* pre_count;
+  const float* pre_dist;
   uint32_t n;
   int* error;
 };
 
+// insertMultipleSearchResults (Index.cpp:673-727) on the device: the batch's
+// pair distances, then per batch object the edgeSizeForCreation best of its
+// search results and the earlier batch objects, by (distance, id).
+struct BatchPairArgs {
+  const uint8_t* rows;           // object rows
+  uint64_t row_bytes;
+  int dp;
+  const uint8_t* batch;          // the batch objects' rows, batch order
+  const uint32_t* ids;           // [n] batch ids
+  uint32_t n;
+  float* out;                    // [n(n-1)/2]: pair (i, j), j < i, at i(i-1)/2 + j
+};
+
+struct BatchMergeArgs {
+  const uint32_t* res_ids;       // [n][K] insertion search results
+  const float* res_dists;
+  const uint32_t* res_n;         // [n]
+  uint32_t K;                    // edgeSizeForCreation
+  const uint32_t* ids;           // [n] batch ids
+  const float* pair;             // BatchPairArgs::out
+  uint32_t n;
+  uint32_t* out_ids;             // [n][K]
+  float* out_dists;
+  uint32_t* out_n;               // [n]
+  uint8_t* flag;                 // [n] DVP-tree insertion flag (Index.cpp:1201-1203)
+};
+
+hipError_t launch_batch_pairs(const BatchPairArgs& a, int metric, int otype, hipStream_t s);
+hipError_t launch_batch_merge(const BatchMergeArgs& a, hipStream_t s);
 hipError_t launch_tree_insert(const TreeBuildArgs& a, int metric, int otype, hipStream_t s);
 hipError_t launch_adj_scatter(uint32_t* adj, uint64_t stride, const uint32_t* nodes, const uint32_t* vals,
                               uint32_t n, hipStream_t s);

@@ -320,6 +320,8 @@ __global__ void __launch_bounds__(64) ngt_qg_adc_kernel(QgAdcArgs a) {
 __device__ __forceinline__ bool visited_test(uint32_t ht_log2, const uint32_t* ht, uint32_t id, bool vis_mode,
                                              const uint8_t* vis, uint32_t epoch) {
   if (vis_mode) {
+    // the LDS table doubles as a cache of visited ids (see visit())
+    if (ht_log2 && ht[ht_hash(id, 32 - ht_log2)] == id) return true;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
     const uint32_t word = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return ((word >> (8 * (id & 3))) & 0xffu) == epoch;

@@ -87,9 +87,18 @@ __device__ __forceinline__ uint32_t ht_hash(uint32_t id, uint32_t shift) {
 __device__ __forceinline__ bool visit(uint32_t ht_log2, SearchState& st, uint32_t id, bool vis_mode,
                                       uint8_t* vis, uint32_t epoch) {
   if (vis_mode) {
+    // With an LDS table (ht_log2 != 0) it stays on as a direct-mapped cache of
+    // visited ids in front of the epoch bytes: only visited ids are ever
+    // written to it, so a hit is exact and a miss falls through to HBM.
+    uint32_t h = 0;
+    if (ht_log2) {
+      h = ht_hash(id, 32 - ht_log2);
+      if (st.ht[h] == id) return false;
+    }
     const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
     const uint32_t word = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t old = (word >> (8 * (id & 3))) & 0xffu;
+    if (ht_log2) st.ht[h] = id;
     if (old == epoch) return false;
     vis[id] = (uint8_t)epoch;
     return true;

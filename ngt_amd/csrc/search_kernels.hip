@@ -109,6 +109,15 @@ __global__ void __launch_bounds__(64) ngt_tree_seed_kernel(TreeSeedArgs a) {
     // leaves as CSR (a loaded index) or fixed-stride rows (the tree under construction)
     const uint64_t b = a.leaf_count ? (uint64_t)lid * a.leaf_stride : a.leaf_off[lid];
     uint32_t n = a.leaf_count ? a.leaf_count[lid] : (uint32_t)(a.leaf_off[lid + 1] - b);
+    if (a.out_leaf) {
+      float pd = 0.f;
+      if (n != 0 && lane < 4) pd = quad_distance<M, T>(qlds, row_ptr<T>(a.leaf_pivot, a.row_bytes, lid), a.dp, lane);
+      if (lane == 0) {
+        a.out_leaf[qi] = lid;
+        a.out_count[qi] = n;
+        a.out_pdist[qi] = pd;
+      }
+    }
     uint32_t* out = a.seeds + (uint64_t)qi * a.seed_stride;
     if (n > a.seed_stride) n = a.seed_stride;
     for (uint32_t i = lane; i < n; i += 64) out[i] = a.leaf_ids[b + i];
@@ -581,7 +590,11 @@ hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint3
     return v ? atoi(v) : 1;
   }();
   if (metric == kL2 && otype == kFloat && (a.dp == 128 || a.dp == 96)) {
-    if (a.dp == 128 && groups == 2)
+    // Small launches (construction batches: 200 queries, under one wave per
+    // CU) are latency-bound: keep 64 rows per wave in flight instead of 16.
+    if (a.dp == 128 && (groups == 4 || (groups == 1 && slots < 512)))
+      hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 8, 4>), dim3(slots), dim3(64), lds, s, a);
+    else if (a.dp == 128 && groups == 2)
       hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 8, 2>), dim3(slots), dim3(64), lds, s, a);
     else if (a.dp == 128)
       hipLaunchKernelGGL((ngt_graph_search_kernel<kL2, float, 8, 1>), dim3(slots), dim3(64), lds, s, a);

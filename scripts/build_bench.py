@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--edges", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=200, help="batchSizeForCreation")
     ap.add_argument("--check", type=int, default=2000, help="nodes whose edge lists are checked")
     ap.add_argument("--queries", type=int, default=200)
     args = ap.parse_args()
@@ -58,14 +59,16 @@ def main():
     ix = DeviceIndex("l2", "float", args.dim)
     ix.set_objects(rows)
     t0 = time.perf_counter()
-    (offs, ids, ds), tree = ix.build_anng(edge_size_for_creation=args.edges)
+    (offs, ids, ds), tree = ix.build_anng(edge_size_for_creation=args.edges,
+                                             batch_size_for_creation=args.batch)
     t1 = time.perf_counter()
     check(offs, ids, ds, tree, rows, args.n, args.check, np.random.default_rng(1))
     ix.set_tree(tree)
     gi, _, _, _ = ix.search(qs, k=10, epsilon=0.1)
     li, _, _ = ix.linear_search(qs, k=10)
     recall = float(np.mean([len(set(gi[i]) & set(li[i])) / 10.0 for i in range(len(qs))]))
-    out = {"n": args.n, "dim": args.dim, "edge_size_for_creation": args.edges, "build_s": t1 - t0,
+    out = {"n": args.n, "dim": args.dim, "edge_size_for_creation": args.edges, "batch": args.batch,
+           "build_s": t1 - t0,
            "objects_per_s": args.n / (t1 - t0), "edges": int(len(ids)),
            "mean_degree": float(len(ids)) / args.n, "recall_at_10_eps0.1": recall}
     print(json.dumps(out))
