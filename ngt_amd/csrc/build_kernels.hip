@@ -191,14 +191,19 @@ __device__ void std_sort(SortItem* first, SortItem* last) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// DVPTree::insert for one batch.  LDS: fs ids / keys / cluster ids / leaf
-// distances (101 each) and the 101 x 101 distance matrix (40.8 KB).
+// DVPTree::insert for one batch, one 256-thread workgroup.  Wave 0 runs the
+// sequential part (descent, duplicate check, append, the bookkeeping of a
+// split); all four waves share a split's distance work.  LDS: fs ids / keys /
+// cluster ids / leaf distances (101 each), sort items, variances, the
+// 101 x 101 distance matrix (40.8 KB) and the batch's leaf replacements.
 // ---------------------------------------------------------------------------
 template <int M, typename T>
-__global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
+__global__ void __launch_bounds__(256) ngt_tree_insert_kernel(TreeBuildArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int lane = lane_id();
-  const int g = lane & 3, quad = lane >> 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int g = tid & 3, bq = tid >> 2;  // 64 quads per workgroup
+  constexpr int kQuads = 64;
   const uint32_t LS = a.leaf_size;  // leafObjectsSize (100)
   uint32_t* fs_id = reinterpret_cast<uint32_t*>(smem);
   float* fs_dist = reinterpret_cast<float*>(fs_id + 128);
@@ -208,8 +213,11 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
   double* var = reinterpret_cast<double*>(items + 128);
   float* D = reinterpret_cast<float*>(var + 128);  // [NF][NF]
   uint32_t* repl_leaf = reinterpret_cast<uint32_t*>(D + (size_t)(LS + 1) * (LS + 1));  // [256]
-  uint32_t* repl_in = repl_leaf + 256;                                         // [256]
-  uint32_t nrepl = 0;
+  uint32_t* repl_in = repl_leaf + 256;                                                 // [256]
+  uint32_t* ctl = repl_in + 256;  // [2][2]: (leaf, fsize) of the split decided for an insert
+  uint32_t nrepl = 0;             // wave 0's copy
+  uint32_t it = 0;                // inserts processed: selects the ctl slot, so wave 0 (at most
+                                  // one barrier ahead) never rewrites the slot the others read
   const uint64_t rb = a.row_bytes;
   auto row = [&](uint32_t id) { return a.rows + (uint64_t)id * rb; };
 
@@ -217,134 +225,133 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
     if (!a.insert_flag[t]) continue;
     const uint32_t id = a.ids[t];
     const uint8_t* q = row(id);
-    // ---- leaf descent (DVPTree::search, SearchLeaf, radius 0) -------------
-    // Pre-located: the leaf found against the tree at batch start is still
-    // on the object's path unless a split of this batch replaced it, and a
-    // split replaces a leaf in place by an internal node whose subtree then
-    // holds the path -- descend from the first such node.  A leaf that was
-    // not empty at batch start keeps its pivot until it splits, so its
-    // pivot distance is the pre-computed one.
-    uint32_t node = a.counts[2];
-    bool have_pd = false;
-    float pre_pd = 0.f;
-    if (a.pre_leaf) {
-      const uint32_t pl = a.pre_leaf[t];
-      node = kLeaf | pl;
-      uint32_t hit = 0xffffffffu;
-      for (uint32_t r0 = 0; r0 < nrepl; r0 += 64) {
-        const uint64_t m = ballot64(r0 + lane < nrepl && repl_leaf[r0 + lane] == pl);
-        if (m) {
-          hit = repl_in[r0 + __ffsll((long long)m) - 1];
+    uint32_t* c2 = ctl + 2 * (it++ & 1);
+    if (w == 0) {
+      do {
+        // ---- leaf descent (DVPTree::search, SearchLeaf, radius 0) -----------
+        // Pre-located: the leaf found against the tree at batch start is still
+        // on the object's path unless a split of this batch replaced it, and a
+        // split replaces a leaf in place by an internal node whose subtree then
+        // holds the path -- descend from the first such node.  A leaf that was
+        // not empty at batch start keeps its pivot until it splits, so its
+        // pivot distance is the pre-computed one.
+        uint32_t node = a.counts[2];
+        bool have_pd = false;
+        float pd = 0.f;
+        if (a.pre_leaf) {
+          const uint32_t pl = a.pre_leaf[t];
+          node = kLeaf | pl;
+          uint32_t hit = 0xffffffffu;
+          for (uint32_t r0 = 0; r0 < nrepl; r0 += 64) {
+            const uint64_t m = ballot64(r0 + lane < nrepl && repl_leaf[r0 + lane] == pl);
+            if (m) {
+              hit = repl_in[r0 + __ffsll((long long)m) - 1];
+              break;
+            }
+          }
+          if (hit != 0xffffffffu) {
+            node = hit;
+          } else if (a.pre_count[t] != 0) {
+            have_pd = true;
+            pd = a.pre_dist[t];
+          }
+        }
+        while (!(node & kLeaf)) {
+          const uint32_t iid = node;
+          const float d = dist1<M, T>(q, a.in_pivot + (uint64_t)iid * rb, a.dp);
+          const float* b = a.in_border + (uint64_t)iid * 4;
+          uint32_t mid = 0;
+          for (; mid < 4; mid++)
+            if (d < b[mid]) break;
+          node = a.in_child[(uint64_t)iid * 5 + mid];
+        }
+        const uint32_t lid = node & ~kLeaf;
+        uint32_t* lids = a.lf_ids + (uint64_t)lid * a.leaf_cap;
+        float* ldst = a.lf_dist + (uint64_t)lid * a.leaf_cap;
+        const uint32_t cnt = a.lf_count[lid];
+        if (lane == 0) c2[1] = 0;
+        // ---- DVPTree::insert(iobj, leaf): duplicate check (Tree.cpp:48-87) ---
+        bool skip = false;
+        if (cnt != 0 && !have_pd) pd = dist1<M, T>(q, a.lf_pivot + (uint64_t)lid * rb, a.dp);
+        if (cnt != 0) {
+          for (uint32_t base = 0; base < cnt && !skip; base += 64) {
+            uint64_t eq = ballot64(base + lane < cnt && ldst[base + lane] == pd);
+            while (eq) {
+              const int j = __ffsll((long long)eq) - 1;
+              eq &= eq - 1;
+              const uint32_t loid = lids[base + j];
+              const float idd = dist1<M, T>(q, row(loid), a.dp);
+              if (idd == 0.0f) {
+                if (loid == id && lane == 0) atomicOr(a.error, 2);  // "already existed"
+                skip = true;
+                break;
+              }
+            }
+          }
+        }
+        if (skip) break;
+        if (cnt < LS) {
+          // ---- insertObject (Tree.cpp:267-313) -------------------------------
+          if (cnt == 0) {
+            copy_row(a.lf_pivot + (uint64_t)lid * rb, q, rb);
+            if (lane == 0) {
+              a.lf_has_pivot[lid] = 1;
+              lids[0] = id;
+              ldst[0] = 0.f;
+              a.lf_count[lid] = 1;
+            }
+          } else if (lane == 0) {
+            lids[cnt] = id;
+            ldst[cnt] = pd;
+            a.lf_count[lid] = cnt + 1;
+          }
           break;
         }
-      }
-      if (hit != 0xffffffffu) {
-        node = hit;
-      } else if (a.pre_count[t] != 0) {
-        have_pd = true;
-        pre_pd = a.pre_dist[t];
-      }
-    }
-    while (!(node & kLeaf)) {
-      const uint32_t iid = node;
-      const float d = dist1<M, T>(q, a.in_pivot + (uint64_t)iid * rb, a.dp);
-      const float* b = a.in_border + (uint64_t)iid * 4;
-      uint32_t mid = 0;
-      for (; mid < 4; mid++)
-        if (d < b[mid]) break;
-      node = a.in_child[(uint64_t)iid * 5 + mid];
-    }
-    const uint32_t lid = node & ~kLeaf;
-    uint32_t* lids = a.lf_ids + (uint64_t)lid * a.leaf_cap;
-    float* ldst = a.lf_dist + (uint64_t)lid * a.leaf_cap;
-    const uint32_t cnt = a.lf_count[lid];
-    // ---- DVPTree::insert(iobj, leaf): duplicate check (Tree.cpp:48-87) -----
-    bool skip = false;
-    float pd = pre_pd;
-    if (cnt != 0 && !have_pd) pd = dist1<M, T>(q, a.lf_pivot + (uint64_t)lid * rb, a.dp);
-    if (cnt != 0) {
-      const float d = pd;
-      for (uint32_t base = 0; base < cnt && !skip; base += 64) {
-        uint64_t eq = ballot64(base + lane < cnt && ldst[base + lane] == d);
-        while (eq) {
-          const int j = __ffsll((long long)eq) - 1;
-          eq &= eq - 1;
-          const uint32_t loid = lids[base + j];
-          const float idd = dist1<M, T>(q, row(loid), a.dp);
-          if (idd == 0.0f) {
-            if (loid == id && lane == 0) atomicOr(a.error, 2);  // "already existed"
-            skip = true;
-            break;
-          }
-        }
-      }
-    }
-    if (skip) continue;
-    if (cnt < LS) {
-      // ---- insertObject (Tree.cpp:267-313) ---------------------------------
-      if (cnt == 0) {
-        copy_row(a.lf_pivot + (uint64_t)lid * rb, q, rb);
+        // ---- split (Tree.cpp:98-117): fs = leaf objects + the new one --------
+        for (uint32_t i = lane; i < cnt; i += 64) fs_id[i] = lids[i];
         if (lane == 0) {
-          a.lf_has_pivot[lid] = 1;
-          lids[0] = id;
-          ldst[0] = 0.f;
-          a.lf_count[lid] = 1;
+          fs_id[cnt] = id;
+          c2[0] = lid;
+          c2[1] = cnt + 1;
         }
-      } else {
-        const float d = pd;
-        if (lane == 0) {
-          lids[cnt] = id;
-          ldst[cnt] = d;
-          a.lf_count[lid] = cnt + 1;
-        }
-      }
-      __threadfence_block();
-      __syncthreads();
-      continue;
+      } while (false);
     }
-    // ---- split (Tree.cpp:98-117): fs = leaf objects + the new one ----------
-    const uint32_t fsize = cnt + 1;
-    for (uint32_t i = lane; i < cnt; i += 64) fs_id[i] = lids[i];
-    if (lane == 0) fs_id[cnt] = id;
     __syncthreads();
+    const uint32_t fsize = c2[1];
+    if (fsize == 0) continue;
+    const uint32_t lid = c2[0];
+
     // selectPivotByMaxVariance (Node.cpp:97-144): D[i][j] = comparator(fs[i], fs[j]), i < j
-    {
-      const uint32_t npairs = fsize * (fsize - 1) / 2;
-      for (uint32_t p0 = 0; p0 < npairs; p0 += 16) {
-        const uint32_t p = p0 + quad;
-        float d = 0.f;
-        uint32_t i = 0, j = 0;
-        if (p < npairs) {
-          // row i holds pairs (i, i+1..fsize-1)
-          uint32_t rem = p;
-          i = 0;
-          while (rem >= fsize - 1 - i) {
-            rem -= fsize - 1 - i;
-            i++;
-          }
-          j = i + 1 + rem;
-          d = quad_dist_rows<M, T>(row(fs_id[i]), row(fs_id[j]), a.dp, g);
-        }
-        if (p < npairs && g == 0) {
-          D[i * fsize + j] = d;
-          D[j * fsize + i] = d;
+    const uint32_t npairs = fsize * (fsize - 1) / 2;
+    for (uint32_t p0 = 0; p0 < npairs; p0 += kQuads) {
+      const uint32_t p = p0 + bq;
+      if (p < npairs) {
+        // p = hi(hi-1)/2 + lo, lo < hi
+        uint32_t hi = (uint32_t)((1.0f + sqrtf(1.0f + 8.0f * (float)p)) * 0.5f);
+        while (hi * (hi - 1) / 2 > p) hi--;
+        while ((hi + 1) * hi / 2 <= p) hi++;
+        const uint32_t lo = p - hi * (hi - 1) / 2;
+        const float d = quad_dist_rows<M, T>(row(fs_id[lo]), row(fs_id[hi]), a.dp, g);
+        if (g == 0) {
+          D[lo * fsize + hi] = d;
+          D[hi * fsize + lo] = d;
         }
       }
-      for (uint32_t i = lane; i < fsize; i += 64) D[i * fsize + i] = 0.f;
-      __syncthreads();
-      for (uint32_t i = lane; i < fsize; i += 64) {
-        double avg = 0.0;
-        for (uint32_t j = 0; j < fsize; j++) avg += (double)D[i * fsize + j];
-        avg /= (double)fsize;
-        double v = 0.0;
-        for (uint32_t j = 0; j < fsize; j++) {
-          const double x = (double)D[i * fsize + j] - avg;
-          v += x * x;  // pow(x, 2.0)
-        }
-        var[i] = v / (double)fsize;
-      }
-      __syncthreads();
     }
+    for (uint32_t i = tid; i < fsize; i += 256) D[i * fsize + i] = 0.f;
+    __syncthreads();
+    for (uint32_t i = tid; i < fsize; i += 256) {
+      double avg = 0.0;
+      for (uint32_t j = 0; j < fsize; j++) avg += (double)D[i * fsize + j];
+      avg /= (double)fsize;
+      double v = 0.0;
+      for (uint32_t j = 0; j < fsize; j++) {
+        const double x = (double)D[i * fsize + j] - avg;
+        v += x * x;  // pow(x, 2.0)
+      }
+      var[i] = v / (double)fsize;
+    }
+    __syncthreads();
     uint32_t pv = 0;
     {
       double maxv = var[0];
@@ -355,31 +362,52 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
         }
     }
     // splitObjects (Node.cpp:146-225): distance from the pivot, sort, clusters
-    for (uint32_t i0 = 0; i0 < fsize; i0 += 16) {
-      const uint32_t i = i0 + quad;
+    for (uint32_t i0 = 0; i0 < fsize; i0 += kQuads) {
+      const uint32_t i = i0 + bq;
       float d = 0.f;
       if (i < fsize && i != pv) d = quad_dist_rows<M, T>(row(fs_id[pv]), row(fs_id[i]), a.dp, g);
       if (i < fsize && g == 0) fs_dist[i] = d;
     }
     __syncthreads();
-    if (lane == 0) {
-      for (uint32_t i = 0; i < fsize; i++) {
-        items[i].d = fs_dist[i];
-        items[i].i = i;
+    // std::sort by distance: with distinct distances every correct sort gives
+    // the same order (rank = number of smaller keys); ties keep libstdc++'s
+    // introsort order, restated step by step on one lane.
+    bool tie = false;
+    if ((uint32_t)tid < fsize) {
+      const float di = fs_dist[tid];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < fsize; j++) {
+        const float dj = fs_dist[j];
+        rank += dj < di ? 1u : 0u;
+        tie |= (dj == di) && j != (uint32_t)tid;
       }
-      std_sort(items, items + fsize);
+      items[rank].d = di;
+      items[rank].i = (uint32_t)tid;
+    }
+    if (__syncthreads_or(tie)) {
+      if (tid == 0) {
+        for (uint32_t i = 0; i < fsize; i++) {
+          items[i].d = fs_dist[i];
+          items[i].i = i;
+        }
+        std_sort(items, items + fsize);
+      }
+      __syncthreads();
+    }
+    // permute fs into sorted order
+    uint32_t sid = 0;
+    float sd = 0.f;
+    if ((uint32_t)tid < fsize) {
+      sid = fs_id[items[tid].i];
+      sd = items[tid].d;
     }
     __syncthreads();
-    // permute fs into sorted order
-    uint32_t sid0 = 0, sid1 = 0;
-    float sd0 = 0.f, sd1 = 0.f;
-    if ((uint32_t)lane < fsize) { sid0 = fs_id[items[lane].i]; sd0 = items[lane].d; }
-    if ((uint32_t)lane + 64 < fsize) { sid1 = fs_id[items[lane + 64].i]; sd1 = items[lane + 64].d; }
+    if ((uint32_t)tid < fsize) {
+      fs_id[tid] = sid;
+      fs_dist[tid] = sd;
+    }
     __syncthreads();
-    if ((uint32_t)lane < fsize) { fs_id[lane] = sid0; fs_dist[lane] = sd0; }
-    if ((uint32_t)lane + 64 < fsize) { fs_id[lane + 64] = sid1; fs_dist[lane + 64] = sd1; }
-    __syncthreads();
-    if (lane == 0) {
+    if (tid == 0) {
       const int csize = 5;
       int cid = csize - 1;
       int cms = ((int)fsize * cid) / csize;
@@ -404,8 +432,8 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
     __syncthreads();
     // leafDistance: -1 (Object::Pivot) for the first of each cluster, else the
     // distance to that first object
-    for (uint32_t i0 = 0; i0 < fsize; i0 += 16) {
-      const uint32_t i = i0 + quad;
+    for (uint32_t i0 = 0; i0 < fsize; i0 += kQuads) {
+      const uint32_t i = i0 + bq;
       float ld = -1.0f;
       if (i < fsize) {
         uint32_t first = i;
@@ -415,94 +443,91 @@ __global__ void __launch_bounds__(64) ngt_tree_insert_kernel(TreeBuildArgs a) {
       if (i < fsize && g == 0) fs_ld[i] = ld;
     }
     __syncthreads();
-    // ---- recombineNodes (Tree.cpp:119-265) --------------------------------
-    const uint32_t targetParent = a.lf_parent[lid];
-    const uint32_t targetId = kLeaf | lid;
-    const uint32_t inid = a.counts[1];
-    const uint32_t nl0 = a.counts[0];
-    if (inid >= a.in_cap_nodes || nl0 + 4 > a.leaf_cap_nodes) {
-      if (lane == 0) atomicOr(a.error, 16);  // capacity
-      return;
-    }
-    uint32_t ln[5] = {lid, nl0, nl0 + 1, nl0 + 2, nl0 + 3};
-    {
-      bool known = false;
-      for (uint32_t r0 = 0; r0 < nrepl; r0 += 64)
-        known |= ballot64(r0 + lane < nrepl && repl_leaf[r0 + lane] == lid) != 0;
-      if (!known && nrepl < 256) {
-        if (lane == 0) {
-          repl_leaf[nrepl] = lid;
-          repl_in[nrepl] = inid;
-        }
-        nrepl++;
-      }
-    }
-    if (lane == 0) {
-      for (int c = 0; c < 5; c++) {
-        a.lf_count[ln[c]] = 0;
-        a.lf_has_pivot[ln[c]] = 0;
-      }
-      if ((targetParent & ~kLeaf) != 0) {
-        uint32_t* ch = a.in_child + (uint64_t)targetParent * 5;
-        for (int c = 0; c < 5; c++)
-          if (ch[c] == targetId) {
-            ch[c] = inid;
-            break;
+    // ---- recombineNodes (Tree.cpp:119-265), wave 0 ------------------------
+    if (w == 0) {
+      const uint32_t targetParent = a.lf_parent[lid];
+      const uint32_t targetId = kLeaf | lid;
+      const uint32_t inid = a.counts[1];
+      const uint32_t nl0 = a.counts[0];
+      if (inid >= a.in_cap_nodes || nl0 + 4 > a.leaf_cap_nodes) {
+        if (lane == 0) atomicOr(a.error, 16);  // capacity: the host grows the arrays first
+      } else {
+        const uint32_t ln[5] = {lid, nl0, nl0 + 1, nl0 + 2, nl0 + 3};
+        bool known = false;
+        for (uint32_t r0 = 0; r0 < nrepl; r0 += 64)
+          known |= ballot64(r0 + lane < nrepl && repl_leaf[r0 + lane] == lid) != 0;
+        if (!known && nrepl < 256) {
+          if (lane == 0) {
+            repl_leaf[nrepl] = lid;
+            repl_in[nrepl] = inid;
           }
-      }
-      a.in_parent[inid] = targetParent;
-      for (int c = 0; c < 4; c++) a.in_border[(uint64_t)inid * 4 + c] = 0.f;
-    }
-    copy_row(a.in_pivot + (uint64_t)inid * rb, row(fs_id[0]), rb);
-    __syncthreads();
-    // cluster pivots (leafDistance == Pivot) and the fs[0] dummies for empty children
-    int maxClusterID = 0;
-    for (uint32_t i = 0; i < fsize; i++) maxClusterID = fs_cl[i] > maxClusterID ? fs_cl[i] : maxClusterID;
-    for (uint32_t i = 0; i < fsize; i++)
-      if (fs_ld[i] == -1.0f) copy_row(a.lf_pivot + (uint64_t)ln[fs_cl[i]] * rb, row(fs_id[i]), rb);
-    for (int c = maxClusterID + 1; c < 5; c++) copy_row(a.lf_pivot + (uint64_t)ln[c] * rb, row(fs_id[0]), rb);
-    if (lane == 0) {
-      int cid = fs_cl[0];
-      if (fs_ld[0] != -1.0f) atomicOr(a.error, 32);  // "illegal pivot"
-      uint32_t* l0 = a.lf_ids + (uint64_t)ln[cid] * a.leaf_cap;
-      float* d0 = a.lf_dist + (uint64_t)ln[cid] * a.leaf_cap;
-      l0[0] = fs_id[0];
-      d0[0] = 0.0f;
-      a.lf_count[ln[cid]] = 1;
-      a.lf_has_pivot[ln[cid]] = 1;
-      a.lf_parent[ln[cid]] = inid;
-      for (uint32_t i = 1; i < fsize; i++) {
-        const int c = fs_cl[i];
-        float ld;
-        if (fs_ld[i] == -1.0f) {
-          a.lf_has_pivot[ln[c]] = 1;
-          ld = 0.0f;
-        } else {
-          ld = fs_ld[i];
+          nrepl++;
         }
-        const uint32_t k = a.lf_count[ln[c]];
-        a.lf_ids[(uint64_t)ln[c] * a.leaf_cap + k] = fs_id[i];
-        a.lf_dist[(uint64_t)ln[c] * a.leaf_cap + k] = ld;
-        a.lf_count[ln[c]] = k + 1;
-        a.lf_parent[ln[c]] = inid;
-        if (c != cid) {
-          a.in_border[(uint64_t)inid * 4 + cid] = fs_dist[i];
-          cid = c;
+        if (lane == 0 && (targetParent & ~kLeaf) != 0) {
+          uint32_t* ch = a.in_child + (uint64_t)targetParent * 5;
+          for (int c = 0; c < 5; c++)
+            if (ch[c] == targetId) {
+              ch[c] = inid;
+              break;
+            }
+        }
+        copy_row(a.in_pivot + (uint64_t)inid * rb, row(fs_id[0]), rb);
+        // cluster pivots (leafDistance == Pivot) and the fs[0] dummies for empty children
+        int maxClusterID = 0;
+        for (uint32_t i = 0; i < fsize; i++) maxClusterID = fs_cl[i] > maxClusterID ? fs_cl[i] : maxClusterID;
+        for (uint32_t i = 0; i < fsize; i++)
+          if (fs_ld[i] == -1.0f) copy_row(a.lf_pivot + (uint64_t)ln[fs_cl[i]] * rb, row(fs_id[i]), rb);
+        for (int c = maxClusterID + 1; c < 5; c++) copy_row(a.lf_pivot + (uint64_t)ln[c] * rb, row(fs_id[0]), rb);
+        if (lane == 0) {
+          if (fs_ld[0] != -1.0f) atomicOr(a.error, 32);  // "illegal pivot"
+          // distribute fs over the cluster leaves; counts and pivot flags in
+          // registers, written once
+          uint32_t kc[5] = {0, 0, 0, 0, 0};
+          uint8_t hp[5] = {0, 0, 0, 0, 0};
+          float border[4] = {0.f, 0.f, 0.f, 0.f};
+          int cid = fs_cl[0];
+          a.lf_ids[(uint64_t)ln[cid] * a.leaf_cap] = fs_id[0];
+          a.lf_dist[(uint64_t)ln[cid] * a.leaf_cap] = 0.0f;
+          kc[cid] = 1;
+          hp[cid] = 1;
+          for (uint32_t i = 1; i < fsize; i++) {
+            const int c = fs_cl[i];
+            float ld;
+            if (fs_ld[i] == -1.0f) {
+              hp[c] = 1;
+              ld = 0.0f;
+            } else {
+              ld = fs_ld[i];
+            }
+            a.lf_ids[(uint64_t)ln[c] * a.leaf_cap + kc[c]] = fs_id[i];
+            a.lf_dist[(uint64_t)ln[c] * a.leaf_cap + kc[c]] = ld;
+            kc[c]++;
+            if (c != cid) {
+              border[cid] = fs_dist[i];
+              cid = c;
+            }
+          }
+          for (int c = maxClusterID + 1; c < 5; c++) {
+            hp[c] = 1;
+            if (c < 4) border[c] = FLT_MAX;
+          }
+          for (int c = 0; c < 5; c++) {
+            a.lf_count[ln[c]] = kc[c];
+            a.lf_has_pivot[ln[c]] = hp[c];
+            a.lf_parent[ln[c]] = inid;
+          }
+          a.in_parent[inid] = targetParent;
+          for (int c = 0; c < 4; c++) a.in_border[(uint64_t)inid * 4 + c] = border[c];
+          uint32_t* ch = a.in_child + (uint64_t)inid * 5;
+          ch[0] = targetId;
+          for (int c = 1; c < 5; c++) ch[c] = kLeaf | ln[c];
+          a.counts[0] = nl0 + 4;
+          a.counts[1] = inid + 1;
+          if ((targetParent & ~kLeaf) == 0) a.counts[2] = inid;  // the root was this leaf
         }
       }
-      for (int c = maxClusterID + 1; c < 5; c++) {
-        a.lf_parent[ln[c]] = inid;
-        a.lf_has_pivot[ln[c]] = 1;
-        if (c < 4) a.in_border[(uint64_t)inid * 4 + c] = FLT_MAX;
-      }
-      uint32_t* ch = a.in_child + (uint64_t)inid * 5;
-      ch[0] = targetId;
-      for (int c = 1; c < 5; c++) ch[c] = kLeaf | ln[c];
-      a.counts[0] = nl0 + 4;
-      a.counts[1] = inid + 1;
-      if ((targetParent & ~kLeaf) == 0) a.counts[2] = inid;  // the root was this leaf
     }
-    __threadfence_block();
+    __threadfence();
     __syncthreads();
   }
 }
@@ -630,9 +655,9 @@ hipError_t launch_tree_insert(const TreeBuildArgs& a, int metric, int otype, hip
   if (a.n == 0) return hipSuccess;
   const uint32_t nf = a.leaf_size + 1;
   const size_t lds = 128 * (4 + 4 + 4 + 4) + 128 * sizeof(SortItem) + 128 * sizeof(double) +
-                     (size_t)nf * nf * sizeof(float) + 2 * 256 * sizeof(uint32_t);
+                     (size_t)nf * nf * sizeof(float) + 2 * 256 * sizeof(uint32_t) + 4 * sizeof(uint32_t);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-#define L_TI(MM, TT) hipLaunchKernelGGL((ngt_tree_insert_kernel<MM, TT>), dim3(1), dim3(64), lds, s, a)
+#define L_TI(MM, TT) hipLaunchKernelGGL((ngt_tree_insert_kernel<MM, TT>), dim3(1), dim3(256), lds, s, a)
   NGT_BUILD_DISPATCH(metric, otype, L_TI);
 #undef L_TI
   return hipGetLastError();

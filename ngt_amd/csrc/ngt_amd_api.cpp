@@ -335,6 +335,14 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   // overflow paths.
   a.ht_log2 = 12;
   a.cq_cap = 1024;
+  // Small launches (construction batches) leave most of the chip idle and
+  // their time is the slowest query's: give each query a larger LDS visited
+  // hash and unchecked array (57 KB, two per CU) so long searches stay out
+  // of the HBM epochs and the HBM spill.
+  if (nq <= 2048 && prm->visited_hash_log2 == 0) {
+    a.ht_log2 = 13;
+    a.cq_cap = 3072;
+  }
   if (prm->visited_hash_log2 < 0) a.ht_log2 = 0;
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
   if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
