@@ -456,7 +456,7 @@ def main():
                        "seeds": "getRandomSeeds (%d)" % args.seed_size,
                        "distance_computations_per_query": float(c[:, 0].mean()),
                        "expansions_per_query": float(c[:, 2].mean()),
-                       "visited_set": "hbm-epochs" if args.visited < 0 else "lds-hash",
+                       "visited_set": "hbm-epochs+lds-filter" if args.visited < 0 else "lds-hash",
                        "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world),
                        "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -71,6 +71,7 @@ struct SearchArgs {
   uint64_t edge_size;            // resolved getEdgeSize()
   uint32_t ht_log2;              // visited hash capacity (log2); 0 = HBM bitmap only
   uint32_t cq_cap;               // unchecked LDS capacity
+  uint32_t vf_log2;              // LDS visited-filter bits (log2) before the HBM epochs; 0 = none
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;              // [nq][k]
   uint32_t* out_n;               // [nq]

@@ -354,6 +354,8 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
   uint8_t* p = smem;
   const bool use_hash = a.ht_log2 != 0;
   st.ht = reinterpret_cast<uint32_t*>(p);
+  st.vf = nullptr;
+  st.vf_shift = 0;
   if (use_hash) p += (size_t)4 << a.ht_log2;
   st.cq = reinterpret_cast<uint64_t*>(p);
   p += (size_t)8 * a.cq_cap;

@@ -67,6 +67,8 @@ __device__ __forceinline__ void eval_batch(const T* qlds, const uint8_t* rows, u
 // ---------------------------------------------------------------------------
 struct SearchState {
   uint32_t* ht;      // visited hash (LDS)
+  uint32_t* vf;      // visited filter bits (LDS) in front of the HBM epochs, or null
+  uint32_t vf_shift; // 32 - log2(filter bits)
   uint64_t* cq;      // unchecked keys (LDS)
   uint64_t* res;     // sorted results (LDS)
   uint32_t* nid;     // staged candidate ids (LDS, 64)
@@ -87,6 +89,19 @@ __device__ __forceinline__ uint32_t ht_hash(uint32_t id, uint32_t shift) {
 __device__ __forceinline__ bool visit(uint32_t ht_log2, SearchState& st, uint32_t id, bool vis_mode,
                                       uint8_t* vis, uint32_t epoch) {
   if (vis_mode) {
+    // LDS filter: one bit per hash of every visited id.  A clear bit proves
+    // the id unvisited, so the HBM probe (a 128-B line fetch for one byte) is
+    // skipped and only the mark is stored; a set bit falls through to the probe.
+    if (st.vf) {
+      const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+      const uint32_t m = 1u << (b & 31);
+      const uint32_t old = atomicOr(st.vf + (b >> 5), m);
+      if (!(old & m)) {
+        if (ht_log2) st.ht[ht_hash(id, 32 - ht_log2)] = id;
+        vis[id] = (uint8_t)epoch;
+        return true;
+      }
+    }
     // With an LDS table (ht_log2 != 0) it stays on as a direct-mapped cache of
     // visited ids in front of the epoch bytes: only visited ids are ever
     // written to it, so a hit is exact and a miss falls through to HBM.
@@ -118,7 +133,13 @@ __device__ inline void ht_to_vis(uint32_t ht_log2, SearchState& st, uint8_t* vis
   const uint32_t n = 1u << ht_log2;
   for (uint32_t i = lane_id(); i < n; i += 64) {
     const uint32_t id = st.ht[i];
-    if (id) vis[id] = (uint8_t)epoch;
+    if (id) {
+      vis[id] = (uint8_t)epoch;
+      if (st.vf) {
+        const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+        atomicOr(st.vf + (b >> 5), 1u << (b & 31));
+      }
+    }
   }
   __threadfence_block();
 }

@@ -172,6 +172,10 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   const bool use_hash = a.ht_log2 != 0;
   st.ht = reinterpret_cast<uint32_t*>(p);
   if (use_hash) p += (size_t)4 << a.ht_log2;
+  st.vf = a.vf_log2 ? reinterpret_cast<uint32_t*>(p) : nullptr;
+  st.vf_shift = 32 - a.vf_log2;
+  const uint32_t vf_words = a.vf_log2 ? (1u << a.vf_log2) / 32 : 0u;
+  p += (size_t)4 * vf_words;
   st.cq = reinterpret_cast<uint64_t*>(p);
   p += (size_t)8 * a.cq_cap;
   st.res = reinterpret_cast<uint64_t*>(p);
@@ -196,6 +200,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
 
     // ---- per-query init -----------------------------------------------
     for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
+    for (uint32_t i = lane; i < vf_words; i += 64) st.vf[i] = 0u;
     load_query<T>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
     // next epoch of this slot's visited bytes; wipe the array every 255 queries
     uint32_t epoch = a.slot_epoch[slot] + 1;
@@ -575,6 +580,7 @@ hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipSt
 
 size_t search_lds_bytes(const SearchArgs& a, int otype) {
   size_t b = (a.ht_log2 ? ((size_t)4 << a.ht_log2) : 0) + (size_t)8 * a.cq_cap;
+  b += a.vf_log2 ? ((size_t)1 << a.vf_log2) / 8 : 0;
   b += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   b += 512;
   b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;

@@ -223,12 +223,20 @@ def _random_graph(n, dim, deg, seed):
     return rows, offs, e.reshape(-1)
 
 
-@pytest.mark.parametrize("ht,cq,adj", [("12", "1024", "1"), ("8", "64", "1"), ("9", "128", "0"),
-                                       ("bitmap", "1024", "1"), ("bitmap", "64", "0")])
+@pytest.mark.parametrize("ht,cq,adj,vf", [("12", "1024", "1", ""), ("8", "64", "1", ""), ("9", "128", "0", ""),
+                                          ("bitmap", "1024", "1", ""), ("bitmap", "64", "0", ""),
+                                          ("bitmap", "512", "1", "0"), ("bitmap", "512", "1", "11"),
+                                          ("8", "64", "1", "11")])
 @pytest.mark.parametrize("dim", [32, 128])
-def test_overflow_paths_exact(monkeypatch, ht, cq, adj, dim):
+def test_overflow_paths_exact(monkeypatch, ht, cq, adj, vf, dim):
+    """LDS-overflow forms of the visited and unchecked sets, forced small:
+    visited hash -> HBM epochs, the LDS visited filter (default 32 Kbit in the
+    epoch mode; vf "0" off, "11" a 2 Kbit filter that saturates, so both its
+    proven-fresh and fall-through paths run), unchecked array -> HBM spill."""
     if ht != "bitmap":
         monkeypatch.setenv("NGT_AMD_HT_LOG2", ht)
+    if vf:
+        monkeypatch.setenv("NGT_AMD_VFILTER", vf)
     monkeypatch.setenv("NGT_AMD_CQ_CAP", cq)
     monkeypatch.setenv("NGT_AMD_ADJ", adj)
     vh = -1 if ht == "bitmap" else 0
