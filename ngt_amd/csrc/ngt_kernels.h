@@ -262,6 +262,7 @@ struct QgSearchArgs {
   float radius;
   uint32_t ht_log2;
   uint32_t cq_cap;
+  uint32_t vf_log2;              // LDS visited-filter bits (log2); 0 = none
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;
   uint32_t* out_n;

@@ -317,9 +317,15 @@ __global__ void __launch_bounds__(64) ngt_qg_adc_kernel(QgAdcArgs a) {
 // Quantized-graph search: one wave per query, persistent over a work counter.
 // ---------------------------------------------------------------------------
 // Visited test without insertion (the QG loop tests before it marks).
-__device__ __forceinline__ bool visited_test(uint32_t ht_log2, const uint32_t* ht, uint32_t id, bool vis_mode,
+__device__ __forceinline__ bool visited_test(uint32_t ht_log2, const SearchState& st, uint32_t id, bool vis_mode,
                                              const uint8_t* vis, uint32_t epoch) {
+  const uint32_t* ht = st.ht;
   if (vis_mode) {
+    // a clear filter bit proves the id unvisited (see visit())
+    if (st.vf) {
+      const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+      if (!((st.vf[b >> 5] >> (b & 31)) & 1u)) return false;
+    }
     // the LDS table doubles as a cache of visited ids (see visit())
     if (ht_log2 && ht[ht_hash(id, 32 - ht_log2)] == id) return true;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
@@ -354,9 +360,11 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
   uint8_t* p = smem;
   const bool use_hash = a.ht_log2 != 0;
   st.ht = reinterpret_cast<uint32_t*>(p);
-  st.vf = nullptr;
-  st.vf_shift = 0;
   if (use_hash) p += (size_t)4 << a.ht_log2;
+  st.vf = a.vf_log2 ? reinterpret_cast<uint32_t*>(p) : nullptr;
+  st.vf_shift = 32 - a.vf_log2;
+  const uint32_t vf_words = a.vf_log2 ? (1u << a.vf_log2) / 32 : 0u;
+  p += (size_t)4 * vf_words;
   st.cq = reinterpret_cast<uint64_t*>(p);
   p += (size_t)8 * a.cq_cap;
   st.res = reinterpret_cast<uint64_t*>(p);
@@ -385,6 +393,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
     if (qi >= a.nq) break;
 
     for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
+    for (uint32_t i = lane; i < vf_words; i += 64) st.vf[i] = 0u;
     load_query<float>(qlds, a.queries + (uint64_t)qi * a.query_bytes, a.dp);
     LaneLut<PPL> L;
     load_lane_lut<PPL>(L, a.lut + (uint64_t)qi * a.lut_stride, npairs);
@@ -496,7 +505,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       for (uint32_t base = 0; base < deg; base += 64) {
         const uint32_t i = base + lane;
         const bool in = i < deg && st.nd[i] <= expr;
-        const bool seen = in && visited_test(a.ht_log2, st.ht, st.nid[i], bitmap_mode, vis, epoch);
+        const bool seen = in && visited_test(a.ht_log2, st, st.nid[i], bitmap_mode, vis, epoch);
         uint64_t cand = ballot64(in && !seen);
         uint64_t acc = 0;
         while (cand) {
@@ -646,6 +655,7 @@ hipError_t launch_qg_adc(const QgAdcArgs& a, hipStream_t s) {
 
 size_t qg_search_lds_bytes(const QgSearchArgs& a) {
   size_t b = (a.ht_log2 ? ((size_t)4 << a.ht_log2) : 0) + (size_t)8 * a.cq_cap;
+  b += a.vf_log2 ? ((size_t)1 << a.vf_log2) / 8 : 0;
   b += 2 * (((size_t)8 * (a.size + 1) + 15) & ~(size_t)15);
   const uint32_t nstage = a.id_stride > a.size ? a.id_stride : a.size;
   b += (size_t)8 * ((nstage + 63) & ~63u);
