@@ -200,6 +200,19 @@ int ngt_amd_build_get_tree(const ngt_amd_index *index, uint32_t *leaf_parent, ui
                            void *leaf_pivot, uint32_t *in_parent, void *in_pivot, uint32_t *in_child,
                            float *in_border);
 
+/* Incremental construction (createIndex inserts only the objects that have no
+ * graph node yet, Index.cpp:618-621, 648-651): after ngt_amd_build_begin, load
+ * the index's existing graph and DVP tree -- the inverse of the two getters
+ * above -- then ngt_amd_build_insert adds the rest.  A node with no edges is
+ * taken as not yet inserted. */
+int ngt_amd_build_set_graph(ngt_amd_index *index, const uint64_t *offsets, const uint32_t *ids,
+                            const float *dists, uint64_t graph_rows);
+int ngt_amd_build_set_tree(ngt_amd_index *index, const uint32_t *leaf_parent, const uint64_t *leaf_off,
+                           const uint32_t *leaf_ids, const float *leaf_dists, const uint8_t *leaf_has_pivot,
+                           const void *leaf_pivot, uint32_t n_leaf, const uint32_t *in_parent,
+                           const void *in_pivot, const uint32_t *in_child, const float *in_border,
+                           uint32_t n_internal, uint32_t root);
+
 /* ---- repository sharding (one shard per GPU) ------------ *
  * Merge of per-shard result lists gathered from every rank (RCCL all-gather
  * over xGMI): the k best (distance, global id) per query, the ordering of

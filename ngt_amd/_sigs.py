@@ -74,6 +74,9 @@ def declare(L):
         "ngt_amd_build_get_graph": (c_int, [vp, vp, vp, vp]),
         "ngt_amd_build_tree_size": (c_int, [vp, u32p, u32p, u64p]),
         "ngt_amd_build_get_tree": (c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "ngt_amd_build_set_graph": (c_int, [vp, vp, vp, vp, c_uint64]),
+        "ngt_amd_build_set_tree": (c_int, [vp, vp, vp, vp, vp, vp, vp, c_uint32, vp, vp, vp, vp, c_uint32,
+                                           c_uint32]),
         "ngt_amd_merge_results_device": (c_int, [c_int, vp, vp, vp, c_uint32, c_uint32, c_uint32, vp, vp, vp, vp,
                                                  vp]),
         "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),

@@ -419,6 +419,76 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   return 0;
 }
 
+extern "C" int ngt_amd_build_set_graph(ngt_amd_index* ix, const uint64_t* offsets, const uint32_t* ids,
+                                       const float* dists, uint64_t graph_rows) {
+  if (!ix || !ix->build || !offsets || graph_rows > ix->nrows) return fail("ngt_amd_build_set_graph: bad arguments");
+  if (offsets[graph_rows] && (!ids || !dists)) return fail("ngt_amd_build_set_graph: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  BuildState& b = *ix->build;
+  const uint64_t S = b.adj_stride;
+  std::vector<uint32_t> adj((size_t)ix->nrows * S, 0u);
+  b.graph_size = 0;
+  for (uint64_t v = 0; v < graph_rows; v++) {
+    const uint64_t e0 = offsets[v], e1 = offsets[v + 1];
+    auto& node = b.graph[v];
+    node.clear();
+    for (uint64_t e = e0; e < e1; e++) {
+      if (ids[e] == 0 || ids[e] >= ix->nrows) return fail("ngt_amd_build_set_graph: edge %u out of range", ids[e]);
+      node.push_back({ids[e], dists[e]});
+      if (e - e0 < S) adj[(size_t)v * S + (e - e0)] = ids[e];
+    }
+    b.in_graph[v] = e1 > e0 ? 1 : 0;
+    if (e1 > e0) b.graph_size = v + 1;
+  }
+  HIP_OK(hipMemcpy(ix->adj.p, adj.data(), adj.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  return 0;
+}
+
+extern "C" int ngt_amd_build_set_tree(ngt_amd_index* ix, const uint32_t* leaf_parent, const uint64_t* leaf_off,
+                                      const uint32_t* leaf_ids, const float* leaf_dists,
+                                      const uint8_t* leaf_has_pivot, const void* leaf_pivot, uint32_t n_leaf,
+                                      const uint32_t* in_parent, const void* in_pivot, const uint32_t* in_child,
+                                      const float* in_border, uint32_t n_internal, uint32_t root) {
+  if (!ix || !ix->build || !leaf_parent || !leaf_off || !leaf_has_pivot || !leaf_pivot || n_leaf < 2 ||
+      n_internal < 1 || (n_internal > 1 && (!in_parent || !in_pivot || !in_child || !in_border)))
+    return fail("ngt_amd_build_set_tree: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  BuildState& b = *ix->build;
+  b.n_leaf = 2;
+  b.n_internal = 1;
+  if (ensure_tree_capacity(ix, b, n_leaf, n_internal)) return -1;
+  const uint64_t rb = ix->row_bytes;
+  std::vector<uint32_t> cnt(n_leaf), lids((size_t)n_leaf * kLeafCap, 0u);
+  std::vector<float> ldst((size_t)n_leaf * kLeafCap, 0.f);
+  for (uint32_t l = 0; l < n_leaf; l++) {
+    const uint64_t c = leaf_off[l + 1] - leaf_off[l];
+    if (c > kLeafCap - 1) return fail("ngt_amd_build_set_tree: leaf %u holds %llu objects", l, (unsigned long long)c);
+    cnt[l] = (uint32_t)c;
+    for (uint64_t j = 0; j < c; j++) {
+      lids[(size_t)l * kLeafCap + j] = leaf_ids[leaf_off[l] + j];
+      ldst[(size_t)l * kLeafCap + j] = leaf_dists ? leaf_dists[leaf_off[l] + j] : 0.f;
+    }
+  }
+  HIP_OK(hipMemcpy(b.lf_count.p, cnt.data(), n_leaf * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b.lf_ids.p, lids.data(), lids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b.lf_dist.p, ldst.data(), ldst.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b.lf_parent.p, leaf_parent, n_leaf * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b.lf_has_pivot.p, leaf_has_pivot, n_leaf, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b.lf_pivot.p, leaf_pivot, (size_t)n_leaf * rb, hipMemcpyHostToDevice));
+  if (n_internal > 1) {
+    HIP_OK(hipMemcpy(b.in_parent.p, in_parent, n_internal * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b.in_pivot.p, in_pivot, (size_t)n_internal * rb, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b.in_child.p, in_child, (size_t)n_internal * 5 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b.in_border.p, in_border, (size_t)n_internal * 4 * sizeof(float), hipMemcpyHostToDevice));
+  }
+  const uint32_t c3[3] = {n_leaf, n_internal, root};
+  HIP_OK(b.counts.upload(c3, 3));
+  b.n_leaf = n_leaf;
+  b.n_internal = n_internal;
+  b.root = root;
+  return 0;
+}
+
 extern "C" int ngt_amd_build_graph_size(const ngt_amd_index* ix, uint64_t* graph_size, uint64_t* nedges) {
   if (!ix || !ix->build || !graph_size || !nedges) return fail("ngt_amd_build_graph_size: bad arguments");
   const BuildState& b = *ix->build;

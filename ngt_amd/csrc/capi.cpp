@@ -199,9 +199,10 @@ std::string build_anng(CapiIndex* ix) {
   if (h.prop.edge_size_for_creation == 0) return "";  // createIndex returns at once (Index.cpp:1162-1164)
   if (h.prop.graph_type != 1) return "index construction supports graphType ANNG only";
   if (h.prop.index_type != 0) return "index construction supports GraphAndTree indexes only";
-  for (uint64_t v = 0; v < h.nrows && v + 1 < h.edge_off.size(); v++)
-    if (h.edge_off[v + 1] != h.edge_off[v])
-      return "incremental construction into an index that already has a graph is not implemented";
+  bool has_graph = false;
+  for (uint64_t v = 0; v < h.nrows && v + 1 < h.edge_off.size() && !has_graph; v++)
+    has_graph = h.edge_off[v + 1] != h.edge_off[v];
+  if (has_graph && !h.tree.present) return "the index has a graph but no DVP tree";
   if (h.nrows < 2) return "";
   std::string e = sync_device(ix);
   if (!e.empty()) return e;
@@ -211,7 +212,21 @@ std::string build_anng(CapiIndex* ix) {
   p.batch_size_for_creation = h.prop.batch_size_for_creation;
   p.seed_size = h.prop.seed_size;
   p.epsilon_for_creation = (float)h.prop.epsilon_for_creation;
-  if (ngt_amd_build_begin(ix->dev, &p) || ngt_amd_build_insert(ix->dev, 1, h.nrows)) return amd_err();
+  if (ngt_amd_build_begin(ix->dev, &p)) return amd_err();
+  if (has_graph) {
+    // incremental: the objects without a node join the existing graph and tree
+    const ngt_amd::HostTree& t = h.tree;
+    const uint32_t nl = (uint32_t)t.leaf_parent.size(), ni = (uint32_t)t.in_parent.size();
+    if (h.edge_off.size() < h.nrows + 1 || h.edge_dists.size() != h.edges.size())
+      return "graph arrays inconsistent with the repository";
+    if (ngt_amd_build_set_graph(ix->dev, h.edge_off.data(), h.edges.data(), h.edge_dists.data(), h.nrows) ||
+        ngt_amd_build_set_tree(ix->dev, t.leaf_parent.data(), t.leaf_off.data(), t.leaf_ids.data(),
+                               t.leaf_dists.data(), t.leaf_has_pivot.data(), t.leaf_pivot.data(), nl,
+                               t.in_parent.data(), t.in_pivot.data(), t.in_child.data(), t.in_border.data(),
+                               ni < 1 ? 1u : ni, t.root))
+      return amd_err();
+  }
+  if (ngt_amd_build_insert(ix->dev, 1, h.nrows)) return amd_err();
   uint64_t gsize = 0, ne = 0;
   if (ngt_amd_build_graph_size(ix->dev, &gsize, &ne)) return amd_err();
   std::vector<uint64_t> off(gsize + 1);

@@ -356,9 +356,13 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     // 32 Kbit LDS filter proves most fresh ids unvisited without their HBM
     // probe, paid for by a 512-key unchecked array (same 9 KB of LDS, 16
     // waves per CU); measured +8 % QPS on C2 at identical results.
+    // Long rows (C3: 3,840 B) dwarf the 128-B probe and their searches
+    // saturate any LDS-sized filter: epochs alone there.
     a.ht_log2 = 0;
-    a.vf_log2 = 15;
-    a.cq_cap = 512;
+    if (ix->row_bytes <= 1024) {
+      a.vf_log2 = 15;
+      a.cq_cap = 512;
+    }
   }
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
   if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));

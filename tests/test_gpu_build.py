@@ -76,3 +76,28 @@ def test_capi_create_index_byte_identical(tmp_path):
         ref = g["ids"][i][g["ids"][i] >= 0]
         assert list(bi[i, :bn[i]]) == list(ref), i
     ix.close()
+
+
+def test_capi_incremental_create_index(tmp_path):
+    """createIndex inserts only the objects without a graph node
+    (Index.cpp:618-621): 2,400 objects built and saved, the index reopened,
+    2,600 more appended and built -- at a batch boundary (200) this is the
+    reference's one-shot build, so the files equal the golden ones."""
+    rows, valid = F.read_obj(os.path.join(GOLD, "c1_anng", "obj"), 128, np.float32)
+    a = str(tmp_path / "a")
+    base.Index.create(a, 128, edge_size_for_creation=10, edge_size_for_search=40)
+    ix = base.Index(a)
+    for i in range(1, 2401):
+        ix.insert_object(rows[i, :128])
+    ix.build_index(8)
+    ix.save(a)
+    ix.close()
+    ix = base.Index(a)
+    for i in range(2401, rows.shape[0]):
+        ix.insert_object(rows[i, :128])
+    ix.build_index(8)
+    out = str(tmp_path / "b")
+    ix.save(out)
+    ix.close()
+    for f in ["obj", "grp", "tre"]:
+        assert filecmp.cmp(os.path.join(out, f), os.path.join(GOLD, "c1_anng", f), shallow=False), f
