@@ -234,13 +234,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
-    ap.add_argument("--visited", type=int, default=-1,
-                    help="visited set: -1 HBM epochs (C2 visits ~1e5 ids/query), 0 LDS hash")
+    ap.add_argument("--visited", type=int, default=-2,
+                    help="visited set: -2 HBM epochs of accepted ids, -1 HBM epochs of every evaluated id "
+                         "(C2 visits ~1e5 ids/query), 0 LDS hash")
     args = ap.parse_args()
     # stdout carries exactly one JSON line: everything else written to fd 1
     # (RCCL's init banner, library chatter) goes to stderr
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if args.mode == "qg" and args.visited == -2:
+        args.visited = -1  # the QG search marks accepted ids only by definition (QuantizedGraph.h:241-266)
     c3 = args.config == "c3"
     if not args.n:
         args.n = 1_250_000 if args.mode == "shard" else 1_000_000
@@ -333,18 +336,19 @@ def main():
         del codes
         log("quantizer + quantized graph in %.1f s (degree <= %d)" % (time.time() - t0, ix.qg_max_degree()))
 
-    def run(eps, si=0):
+    def run(eps, si=0, visited=None):
         oi, od, on, oc = bufs[si]
+        visited = args.visited if visited is None else visited
         if args.mode == "qg":
             ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
                                 oc.data_ptr(), k=K, epsilon=eps, result_expansion=args.expansion,
                                 seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
-                                stream=streams[si], visited_hash_log2=args.visited)
+                                stream=streams[si], visited_hash_log2=visited)
             return
         ix.search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
                          oc.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
                          d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=streams[si],
-                         visited_hash_log2=args.visited)
+                         visited_hash_log2=visited)
         if shard:
             result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
 
@@ -397,6 +401,24 @@ def main():
     qps = NQ * (1 if shard else world) * args.steps / elapsed
 
     c = cnt.cpu().numpy().astype(np.float64)
+    evals_per_query = None
+    if args.mode != "qg" and args.visited == -2:
+        # The timed runs keep only accepted ids in the visited set, so their
+        # counters include re-evaluations of rejected neighbours.  One more
+        # run with every evaluated id in the set gives the reference's distinct
+        # distance count U(q) for the algorithmic bytes -- and must return
+        # exactly the same ids and distances.
+        evals_per_query = float(c[:, 0].mean())
+        fast = [t.clone() for t in (out_i, out_d, out_n)]
+        run(chosen, 0, visited=-1)
+        torch.cuda.synchronize()
+        same = (torch.equal(fast[0], out_i) and torch.equal(fast[1].view(torch.int32), out_d.view(torch.int32))
+                and torch.equal(fast[2], out_n))
+        if not same:
+            raise SystemExit("bench: accepted-only visited set changed the results")
+        log("accepted-only visited set: results identical; %.0f evaluations/query vs %.0f distinct" % (
+            evals_per_query, float(cnt[:, 0].double().mean())))
+        c = cnt.cpu().numpy().astype(np.float64)
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     graph = "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg)
     if args.mode == "qg":
@@ -409,7 +431,7 @@ def main():
         alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + NQ * (dp * 4 + K * 8)
         kname = "ngt_graph_search_kernel"
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = measured_traffic(args.mode, args.config, graph, chosen)
+    traffic = measured_traffic(args.mode, args.config, graph, chosen, args.visited)
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
         tot = c[:, [5, 6, 7, 3]].mean(0)
         log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
@@ -456,7 +478,8 @@ def main():
                        "seeds": "getRandomSeeds (%d)" % args.seed_size,
                        "distance_computations_per_query": float(c[:, 0].mean()),
                        "expansions_per_query": float(c[:, 2].mean()),
-                       "visited_set": "hbm-epochs+lds-filter" if args.visited < 0 else "lds-hash",
+                       "visited_set": {-2: "hbm-epochs+lds-filter, accepted ids only",
+                                       -1: "hbm-epochs+lds-filter"}.get(args.visited, "lds-hash"),
                        "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world),
                        "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -472,12 +495,14 @@ def main():
             line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
         else:
             line["config"]["edges_read_per_query"] = float(c[:, 4].mean())
+            if evals_per_query is not None:
+                line["config"]["evaluations_per_query"] = evals_per_query
         print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def measured_traffic(mode, config, graph, eps):
+def measured_traffic(mode, config, graph, eps, visited):
     """HBM bytes per launch of the search kernel from the committed PMC passes
     (profiles/traffic.json, written from rocprofv3 FETCH_SIZE/WRITE_SIZE) for this
     exact workload and epsilon; NGT_BENCH_TRAFFIC_BYTES overrides; else None."""
@@ -491,7 +516,7 @@ def measured_traffic(mode, config, graph, eps):
         return None
     for e in entries:
         if (e.get("mode", "exact") == mode and e.get("config", "c2") == config and e["graph"] == graph
-                and abs(e["epsilon"] - eps) < 1e-7):
+                and e.get("visited", -1) == visited and abs(e["epsilon"] - eps) < 1e-7):
             return float(e["traffic_bytes"])
     return None
 

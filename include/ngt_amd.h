@@ -76,7 +76,12 @@ typedef struct {
   int32_t visited_hash_log2; /* visited set: 0 = default LDS hash (2^12 ids, spills
                                 exactly to an HBM bitmap), 8..15 = LDS hash of that
                                 size, -1 = HBM bitmap from the start (for searches
-                                that visit far more ids than an LDS hash holds)  */
+                                that visit far more ids than an LDS hash holds),
+                                -2 = as -1 but the set holds only ids that entered
+                                the unchecked set: identical results, fewer HBM
+                                probes; rejected neighbours met again are
+                                re-evaluated, so counters[0] counts evaluations,
+                                not the reference's distinct distance count    */
   int32_t reserved;
 } ngt_amd_search_params;
 

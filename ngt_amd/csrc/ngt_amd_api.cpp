@@ -362,11 +362,18 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     if (ix->row_bytes <= 1024) {
       a.vf_log2 = 15;
       a.cq_cap = 512;
+      // -2: the filter and epochs hold accepted ids only (a few thousand per
+      // query instead of ~7e4), so the filter stays sparse and almost no
+      // neighbour costs an HBM probe or a mark store; rejected neighbours met
+      // again are re-evaluated (search_common.h: not_accepted).  C2: +33 % QPS
+      // at identical results for +14 % distance evaluations.
+      a.accepted_only = prm->visited_hash_log2 == -2;
     }
   }
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
   if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
   if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+  if (const char* v = getenv("NGT_AMD_ACCEPTED_ONLY")) a.accepted_only = atoi(v) != 0;
   if (const char* v = getenv("NGT_AMD_VFILTER")) {
     const int f = atoi(v);
     a.vf_log2 = f <= 0 ? 0u : (uint32_t)std::max(11, std::min(18, f));

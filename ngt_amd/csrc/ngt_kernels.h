@@ -72,6 +72,7 @@ struct SearchArgs {
   uint32_t ht_log2;              // visited hash capacity (log2); 0 = HBM bitmap only
   uint32_t cq_cap;               // unchecked LDS capacity
   uint32_t vf_log2;              // LDS visited-filter bits (log2) before the HBM epochs; 0 = none
+  uint32_t accepted_only;        // epochs/filter hold only ids that entered the unchecked set
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;              // [nq][k]
   uint32_t* out_n;               // [nq]

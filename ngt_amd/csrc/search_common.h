@@ -128,6 +128,28 @@ __device__ __forceinline__ bool visit(uint32_t ht_log2, SearchState& st, uint32_
   }
 }
 
+// Accepted-only visited set (SearchArgs::accepted_only).  The filter and the
+// epoch bytes hold only ids that entered the unchecked set (the seeds and every
+// neighbour with d <= explorationRadius).  A neighbour outside that set is
+// evaluated even if it was evaluated before: it was rejected then with
+// d > explorationRadius, the radius only shrinks, so it is rejected again and
+// the traversal and results are the reference's (Graph.cpp:462-483); only the
+// distance count grows by the re-evaluations.  True <=> evaluate `id`.
+__device__ __forceinline__ bool not_accepted(const SearchState& st, uint32_t id, const uint8_t* vis,
+                                             uint32_t epoch) {
+  const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+  if (!(st.vf[b >> 5] & (1u << (b & 31)))) return true;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(vis + (id & ~3u));
+  const uint32_t word = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ((word >> (8 * (id & 3))) & 0xffu) != epoch;
+}
+
+__device__ __forceinline__ void mark_accepted(SearchState& st, uint32_t id, uint8_t* vis, uint32_t epoch) {
+  const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+  st.vf[b >> 5] |= 1u << (b & 31);
+  vis[id] = (uint8_t)epoch;
+}
+
 // Move the LDS hash contents into the slot's epoch array (exact overflow path).
 __device__ inline void ht_to_vis(uint32_t ht_log2, SearchState& st, uint8_t* vis, uint32_t epoch) {
   const uint32_t n = 1u << ht_log2;

@@ -216,6 +216,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       qfold = query_sq_fold(reinterpret_cast<const float*>(qlds), a.dp);
 
     bool bitmap_mode = !use_hash;
+    const bool lazy = a.accepted_only && !use_hash && st.vf;
     uint32_t nvisited = 0;
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0;
@@ -315,7 +316,8 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         if ((uint32_t)lane < cnt) id = padded ? a.adj[eb + base + lane] : a.edges[eb + base + lane];
         const uint64_t vmask = ballot64(id != 0u);
         nedge += (uint64_t)__popcll(vmask);
-        const bool fresh = id != 0u && visit(a.ht_log2, st, id, bitmap_mode, vis, epoch);
+        const bool fresh = id != 0u && (lazy ? not_accepted(st, id, vis, epoch)
+                                             : visit(a.ht_log2, st, id, bitmap_mode, vis, epoch));
         const uint64_t fmask = ballot64(fresh);
         const uint32_t m = (uint32_t)__popcll(fmask);
         if (fresh) st.nid[mbcnt(fmask)] = id;
@@ -337,6 +339,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
             const float d = st.nd[j];
             if (!(d <= expr)) continue;
             const uint64_t key = make_key(d, st.nid[j]);
+            if (lazy && lane == 0) mark_accepted(st, st.nid[j], vis, epoch);
             if (ncq >= a.cq_cap) {
               ncq = compact(st.cq, ncq, expr);
               if (nspill) nspill = compact(spill, nspill, expr);

@@ -261,6 +261,56 @@ def test_overflow_paths_exact(monkeypatch, ht, cq, adj, vf, dim):
     ix.close()
 
 
+@pytest.mark.parametrize("cq,vf", [("512", ""), ("64", ""), ("512", "11"), ("64", "11")])
+@pytest.mark.parametrize("dim", [32, 128])
+def test_accepted_only_visited_exact(monkeypatch, cq, vf, dim):
+    """visited_hash_log2 = -2: the HBM epochs and the LDS filter hold only
+    accepted ids (seeds and neighbours within the exploration radius); rejected
+    neighbours met again are re-evaluated.  Ids and distances must equal the
+    restatement's exactly, including negative epsilon (exploration radius
+    below the result radius), a finite search radius, HBM spill of the
+    unchecked set (cq 64) and a saturated filter (vf 11); evaluations can
+    only exceed the reference's distinct distance count."""
+    if vf:
+        monkeypatch.setenv("NGT_AMD_VFILTER", vf)
+    monkeypatch.setenv("NGT_AMD_CQ_CAP", cq)
+    n, deg = 3000, 24
+    rows, offs, edges = _random_graph(n, dim, deg, 12)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(4)
+    qs = rng.random((24, dim), dtype=np.float32)
+    seeds = [rng.choice(np.arange(1, n), 10, replace=False).astype(np.uint32) for _ in range(24)]
+    radius = float(np.sqrt(dim / 6.0))  # about the median distance of U[0,1) rows
+    for eps, rad in [(0.0, -1.0), (0.3, -1.0), (1.0, -1.0), (-0.05, -1.0), (0.2, radius)]:
+        gi, gd, gn, cnt = ix.search(qs, k=20, epsilon=eps, radius=rad, edge_size=0, seed_mode=SEED_GIVEN,
+                                    seeds=seeds, visited_hash_log2=-2)
+        for i in range(24):
+            kw = {} if rad < 0 else {"radius": rad}
+            oid, od, ocnt = O.search("l2", rows, offs, edges, qs[i], seeds[i], 20, np.float32(eps), **kw)
+            assert list(gi[i, :gn[i]]) == list(oid), (eps, rad, i)
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32)), (eps, rad, i)
+            assert int(cnt[i, 0]) >= int(ocnt[0])
+    ix.close()
+
+
+def test_accepted_only_visited_reference_index():
+    """visited_hash_log2 = -2 on the reference-built C1 ONNG with tree seeds:
+    identical to the default visited set, whose results the tests above pin to
+    the reference's own (tests/golden/c1_onng)."""
+    ix = device_index("c1_onng")[0]
+    qs = queries()[:64]
+    for eps in [0.0, 0.1]:
+        gi, gd, gn, _ = ix.search(qs, k=10, epsilon=eps, seed_mode=SEED_TREE, visited_hash_log2=-2)
+        ri, rd, rn, _ = ix.search(qs, k=10, epsilon=eps, seed_mode=SEED_TREE, visited_hash_log2=0)
+        assert np.array_equal(gn, rn)
+        for i in range(len(qs)):
+            assert list(gi[i, :gn[i]]) == list(ri[i, :rn[i]]), (eps, i)
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), rd[i, :rn[i]].view(np.uint32))
+    ix.close()
+
+
 def test_edge_cases():
     rows, offs, edges = _random_graph(500, 16, 8, 5)
     ix = DeviceIndex("l2", "float", 16)
