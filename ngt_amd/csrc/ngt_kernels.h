@@ -264,6 +264,7 @@ struct QgSearchArgs {
   uint32_t ht_log2;
   uint32_t cq_cap;
   uint32_t vf_log2;              // LDS visited-filter bits (log2); 0 = none
+  uint32_t two_trips;            // A/B switch: ids, then codes (no combined round trip)
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;
   uint32_t* out_n;

@@ -273,12 +273,14 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   a.cq_cap = 1024;
   a.vf_log2 = 0;
   if (prm->visited_hash_log2 < 0) {
-    // HBM epochs.  The LDS visited filter of run_search does not pay here
-    // (only in-radius candidates are probed) and is left off; a 512-key
-    // unchecked array compacts dead keys twice as often, so pops scan fewer
-    // (+6 % QPS on the C2-graph NGTQG bench, same results).
+    // HBM epochs.  A 512-key unchecked array compacts dead keys twice as
+    // often, so pops scan fewer (+6 % QPS on the C2-graph NGTQG bench, same
+    // results).  The 16 Kbit LDS filter of accepted ids (~1.7k per query)
+    // lets ids_and_adc probe the few possibly-visited neighbours while the
+    // ADC runs, instead of a round trip in the accept step.
     a.ht_log2 = 0;
     a.cq_cap = 512;
+    a.vf_log2 = 14;
   }
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
   if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
@@ -287,6 +289,7 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
     const int f = atoi(v);
     a.vf_log2 = f <= 0 ? 0u : (uint32_t)std::max(11, std::min(18, f));
   }
+  if (const char* v = getenv("NGT_AMD_QG_TWO_TRIPS")) a.two_trips = atoi(v) != 0;
   a.out_ids = d_ids;
   a.out_dists = d_dists;
   a.out_n = d_n;

@@ -290,6 +290,81 @@ __device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* c
   }
 }
 
+// One expansion's neighbour ids and code blocks in a single memory round trip:
+// the loads of the 0-terminated id row and of all `nbs` = id_stride/16 code
+// blocks (<= NB) are issued together, before the degree is known; blocks past
+// the degree are then skipped (their bytes were fetched for nothing, ~10 % of
+// the code traffic at degree ~115 of 128, for one HBM latency less).
+// Returns the degree; ids land in nid[0..id_stride), ADC distances in dists.
+// With `probe` (HBM-epoch visited set behind an LDS filter of accepted ids),
+// the epoch bytes of every neighbour whose filter bit is set are loaded as
+// soon as the ids arrive, under the ADC arithmetic, and seen[c] returns the
+// visited mask of id chunk c -- so the accept step needs no round trip of its
+// own.  A clear filter bit proves an id unvisited (nothing loaded).
+template <int PPL, int NB>
+__device__ __forceinline__ uint32_t ids_and_adc(const LaneLut<PPL>& L, const uint32_t* nbr, uint32_t id_stride,
+                                                const uint8_t* codes, uint32_t Me, float scale, float toff,
+                                                uint32_t* nid, float* dists, bool probe, const SearchState& st,
+                                                const uint8_t* vis, uint32_t epoch, uint64_t (&seen)[2]) {
+  const int lane = lane_id();
+  const uint32_t npairs = Me >> 1;
+  const uint64_t blk = (uint64_t)8 * Me;
+  const uint32_t nbs = id_stride >> 4;
+  uint4 c[NB][PPL];
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+#pragma unroll
+    for (int s = 0; s < PPL; s++) {
+      const uint32_t p = (uint32_t)lane + 64u * s;
+      c[j][s] = make_uint4(0, 0, 0, 0);
+      if ((uint32_t)j < nbs && p < npairs)
+        c[j][s] = *reinterpret_cast<const uint4*>(codes + (uint64_t)j * blk + (uint64_t)p * 16);
+    }
+  }
+  static_assert(NB <= 8, "two 64-id chunks at most");
+  constexpr int NC = (16 * NB + 63) / 64;
+  uint32_t deg = 0;
+  uint32_t idr[NC];
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) {
+    const uint32_t j = 64u * cc;
+    const uint32_t id = j + lane < id_stride ? nbr[j + lane] : 0u;
+    idr[cc] = id;
+    if (j < id_stride) nid[j + lane] = id;
+    deg += (uint32_t)__popcll(ballot64(id != 0u));
+  }
+  bool pre[NC];
+  uint32_t word[NC];
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) {
+    pre[cc] = false;
+    word[cc] = 0;
+    if (probe && idr[cc] != 0u) {
+      const uint32_t b = (idr[cc] * 0x85EBCA77u) >> st.vf_shift;
+      pre[cc] = (st.vf[b >> 5] >> (b & 31)) & 1u;
+      if (pre[cc])
+        word[cc] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (idr[cc] & ~3u)), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  const uint32_t nb = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    if ((uint32_t)j < nb) {
+      uint32_t v[16];
+      block_partials<PPL>(L, c[j], v);
+      const uint32_t r = reduce_scatter16(v);
+      const uint32_t o = (uint32_t)j * 16 + qg_obj_of_lane(lane);
+      if ((lane & 3) == 0 && o < deg) dists[o] = adc_epilogue(r, scale, toff);
+    }
+  }
+  seen[0] = seen[1] = 0;
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++)
+    seen[cc] = ballot64(pre[cc] && ((word[cc] >> (8 * (idr[cc] & 3))) & 0xffu) == epoch);
+  return deg;
+}
+
 // Standalone ADC: wave per (query, node) pair; out[i*out_stride + j] for the
 // node's neighbours j (full list, the QG loop's call at QuantizedGraph.h:240).
 template <int PPL>
@@ -352,7 +427,9 @@ __device__ __forceinline__ void qg_exact(const float* qlds, const QgSearchArgs& 
   }
 }
 
-template <int PPL, int NCH>
+// NB > 0: id rows of up to 16*NB entries load together with all their code
+// blocks (ids_and_adc); NB = 0: ids, then the codes of the degree read.
+template <int PPL, int NCH, int NB>
 __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = lane_id();
@@ -487,13 +564,22 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       const uint32_t target = key_id(wbest);
       const uint32_t* nbr = a.qids + (uint64_t)target * a.id_stride;
       uint32_t deg = 0;
-      for (uint32_t j = 0; j < a.id_stride; j += 64) {
-        const uint32_t id = j + lane < a.id_stride ? nbr[j + lane] : 0u;
-        st.nid[j + lane] = id;
-        deg += (uint32_t)__popcll(ballot64(id != 0u));
+      uint64_t seen_pre[2] = {0, 0};
+      const bool early = NB > 0 && a.id_stride <= 16u * NB && !a.two_trips;
+      const bool probe = early && !use_hash && st.vf != nullptr;
+      if (early) {
+        deg = ids_and_adc<PPL, (NB > 0 ? NB : 1)>(L, nbr, a.id_stride, a.qcodes + (uint64_t)target * a.code_stride,
+                                                  a.Me, scale, toff, st.nid, st.nd, probe, st, vis, epoch, seen_pre);
+        NGT_MARK(t_ids);
+      } else {
+        for (uint32_t j = 0; j < a.id_stride; j += 64) {
+          const uint32_t id = j + lane < a.id_stride ? nbr[j + lane] : 0u;
+          st.nid[j + lane] = id;
+          deg += (uint32_t)__popcll(ballot64(id != 0u));
+        }
+        NGT_MARK(t_ids);
+        adc_node<PPL>(L, a.qcodes + (uint64_t)target * a.code_stride, a.Me, deg, scale, toff, st.nd);
       }
-      NGT_MARK(t_ids);
-      adc_node<PPL>(L, a.qcodes + (uint64_t)target * a.code_stride, a.Me, deg, scale, toff, st.nd);
       __syncthreads();
       NGT_MARK(t_adc);
       nadc += deg;
@@ -505,7 +591,8 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       for (uint32_t base = 0; base < deg; base += 64) {
         const uint32_t i = base + lane;
         const bool in = i < deg && st.nd[i] <= expr;
-        const bool seen = in && visited_test(a.ht_log2, st, st.nid[i], bitmap_mode, vis, epoch);
+        const bool seen = in && (probe ? ((((base == 0) ? seen_pre[0] : seen_pre[1]) >> lane) & 1ull) != 0
+                                       : visited_test(a.ht_log2, st, st.nid[i], bitmap_mode, vis, epoch));
         uint64_t cand = ballot64(in && !seen);
         uint64_t acc = 0;
         while (cand) {
@@ -666,20 +753,20 @@ size_t qg_search_lds_bytes(const QgSearchArgs& a) {
 hipError_t launch_qg_search(const QgSearchArgs& a, uint32_t slots, hipStream_t s) {
   if (a.nq == 0) return hipSuccess;
   const size_t lds = qg_search_lds_bytes(a);
-#define L_QG(P, N) hipLaunchKernelGGL((ngt_qg_search_kernel<P, N>), dim3(slots), dim3(64), lds, s, a)
+#define L_QG(P, N, B) hipLaunchKernelGGL((ngt_qg_search_kernel<P, N, B>), dim3(slots), dim3(64), lds, s, a)
   const int ppl = ppl_of(a.Me);
   if (a.dp == 128) {
     switch (ppl) {
-      case 1: L_QG(1, 8); break;
-      case 2: L_QG(2, 8); break;
-      case 4: L_QG(4, 8); break;
+      case 1: L_QG(1, 8, 8); break;
+      case 2: L_QG(2, 8, 4); break;
+      case 4: L_QG(4, 8, 0); break;
       default: return hipErrorInvalidValue;
     }
   } else {
     switch (ppl) {
-      case 1: L_QG(1, 0); break;
-      case 2: L_QG(2, 0); break;
-      case 4: L_QG(4, 0); break;
+      case 1: L_QG(1, 0, 8); break;
+      case 2: L_QG(2, 0, 4); break;
+      case 4: L_QG(4, 0, 0); break;
       default: return hipErrorInvalidValue;
     }
   }
