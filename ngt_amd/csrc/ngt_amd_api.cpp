@@ -253,7 +253,11 @@ ngt_amd::SearchCtx* ngt_amd::ctx_for(ngt_amd_index* ix, hipStream_t s) {
 
 int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds, hipStream_t s) {
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
-  if (per_cu > 16) per_cu = 16;
+  static const uint32_t max_per_cu = [] {
+    const char* v = getenv("NGT_AMD_WAVES_PER_CU");
+    return v ? (uint32_t)std::max(1, std::min(32, atoi(v))) : 16u;
+  }();
+  if (per_cu > max_per_cu) per_cu = max_per_cu;
   if (per_cu < 1) per_cu = 1;
   uint64_t stride = (ix->nrows + 15) & ~15ull;
   // the per-slot visited epochs take slots * nrows bytes: keep them <= 16 GiB
