@@ -142,31 +142,6 @@ def build_graph(torch, X, knn_k, out_deg, in_deg, max_deg, dev, cosine=False, ch
     return offsets, edges
 
 
-def quantize_dsub1(torch, X, iters=12, sample=100_000):
-    """NGTQG codebooks for dsub = 1 (QuantizedGraph.h:374-385: D <= 400): 16
-    centroids per dimension by Lloyd iterations on a sample (setup only), the
-    global centroid is the zero vector (:397-399).  Returns local [M,16,1] and
-    codes [N, M] (localID - 1) of the objects."""
-    N, D = X.shape
-    g = torch.Generator(device=X.device).manual_seed(7)
-    idx = torch.randint(0, N, (min(sample, N),), device=X.device, generator=g)
-    S = X[idx]                                                     # [s, D]
-    qs = (torch.arange(16, device=X.device, dtype=torch.float32) + 0.5) / 16
-    C = torch.quantile(S, qs, dim=0).t().contiguous()              # [D, 16]
-    for _ in range(iters):
-        a = (S.t()[:, :, None] - C[:, None, :]).abs().argmin(2)    # [D, s]
-        for c in range(16):
-            m = (a == c).float()
-            cnt = m.sum(1)
-            C[:, c] = torch.where(cnt > 0, (m * S.t()).sum(1) / cnt.clamp_min(1), C[:, c])
-        C, _ = C.sort(1)
-    codes = torch.empty((N, D), dtype=torch.uint8, device=X.device)
-    for s in range(0, N, 65536):
-        e = min(N, s + 65536)
-        codes[s:e] = (X[s:e, :, None] - C[None]).abs().argmin(2).to(torch.uint8)
-    return C[:, :, None].contiguous(), codes
-
-
 def random_seeds(nrows, nq, seed_size):
     """GraphIndex::getRandomSeeds (lib/NGT/Index.h:775-801) over the process
     rand() stream (the reference never reseeds it for graph-only search)."""
@@ -327,14 +302,16 @@ def main():
     result = {"ids": out_i}
 
     if args.mode == "qg":
+        # ngtqg quantize on the device: codebooks (dsub = 1, 16 centroids,
+        # 1600-object sample as the reference's dynamic k-means), encoder,
+        # quantized graph (QuantizedGraph.h:456-475)
         t0 = time.time()
-        local_cb, codes = quantize_dsub1(torch, rows[1:, :D])
-        h_codes = np.zeros((N + 1, D), np.uint8)
-        h_codes[1:] = codes.cpu().numpy()
-        ix.qg_set_quantizer(np.zeros(D, np.float32), local_cb.cpu().numpy())
-        ix.qg_build_graph(h_codes, args.qg_edges)
-        del codes
-        log("quantizer + quantized graph in %.1f s (degree <= %d)" % (time.time() - t0, ix.qg_max_degree()))
+        _, its = ix.qg_train(D, nsample=1600, max_iter=20)
+        ix.qg_encode(return_codes=False)
+        ix.qg_build_graph(None, args.qg_edges)
+        torch.cuda.synchronize()
+        log("quantizer (k-means %d-%d iterations) + encoder + quantized graph in %.1f s (degree <= %d)" % (
+            its.min(), its.max(), time.time() - t0, ix.qg_max_degree()))
 
     def run(eps, si=0, visited=None):
         oi, od, on, oc = bufs[si]

@@ -257,9 +257,27 @@ typedef struct {
 /* global: [dimension] floats; local: [M][16][dsub] floats (local ids 1..16). */
 int ngt_amd_qg_set_quantizer(ngt_amd_index *index, const float *global, const float *local,
                              uint32_t M, uint32_t dsub);
-/* local_codes: [nrows][M] bytes, localID - 1 (0..15) of every object (qg/ivt);
+/* local_codes: [nrows][M] bytes, localID - 1 (0..15) of every object (qg/ivt),
+ * or NULL for the codes of the last ngt_amd_qg_encode (kept in HBM);
  * node v keeps its first min(degree, max_edges) graph edges. */
 int ngt_amd_qg_build_graph(ngt_amd_index *index, const uint8_t *local_codes, uint32_t max_edges);
+/* Encoder <- the local half of Quantizer::insert (lib/NGT/NGTQ/Quantizer.h:
+ * 1895-1959, residuals :1407-1435, nearest centroid by the codebook index's
+ * insertion search :1678-1719): every object row 1..nrows-1 coded as its
+ * nearest local centroid per subspace (dsub <= 16), ties to the lower id.
+ * Codes stay in HBM for ngt_amd_qg_build_graph(NULL); codes_out (nullable):
+ * [nrows][M] bytes, localID - 1, row 0 zero. */
+int ngt_amd_qg_encode(ngt_amd_index *index, uint8_t *codes_out);
+/* Local codebook training for NGTQG (ngtqg quantize, QuantizedGraph.h:423-475):
+ * global centroid = the zero vector (:397-399), M subspaces of dim/M (<= 16),
+ * 16 centroids each by Lloyd iterations over objects 1..nsample (<= 4096;
+ * the reference samples 16 * 100), initialised from the first 16 (Head).
+ * The reference clusters with kmeansWithNGT (approximate NGT assignment), so
+ * its codebooks are not reproduced bit for bit.  Installs the quantizer like
+ * ngt_amd_qg_set_quantizer; local_out (nullable): [M][16][dsub]; iters_out
+ * (nullable): [M] iterations run. */
+int ngt_amd_qg_train(ngt_amd_index *index, uint32_t M, uint32_t nsample, uint32_t max_iter, float *local_out,
+                     uint32_t *iters_out);
 /* Node v: neighbour ids qids[qoff[v] .. qoff[v+1]) and packed 4-bit codes
  * codes[code_off[v] .. code_off[v+1]) in the reference stream layout. */
 int ngt_amd_qg_set_graph(ngt_amd_index *index, const uint64_t *qoff, const uint32_t *qids,

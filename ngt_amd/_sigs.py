@@ -81,6 +81,8 @@ def declare(L):
                                                  vp]),
         "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),
         "ngt_amd_qg_build_graph": (c_int, [vp, vp, c_uint32]),
+        "ngt_amd_qg_encode": (c_int, [vp, vp]),
+        "ngt_amd_qg_train": (c_int, [vp, c_uint32, c_uint32, c_uint32, vp, vp]),
         "ngt_amd_qg_set_graph": (c_int, [vp, vp, vp, vp, vp]),
         "ngt_amd_qg_max_degree": (c_uint32, [vp]),
         "ngt_amd_qg_code_stride": (c_uint64, [vp]),

@@ -57,6 +57,8 @@ struct QgState {
   DevBuf<float> local;      // [M][16][dsub]
   DevBuf<uint32_t> qids;    // [nrows][id_stride]
   DevBuf<uint8_t> qcodes;   // [nrows][code_stride]
+  DevBuf<uint8_t> codes;    // [nrows][M] local codes of the last ngt_amd_qg_encode
+  bool has_codes = false;
   uint32_t id_stride = 0;
   uint64_t code_stride = 0;
   bool has_graph = false;

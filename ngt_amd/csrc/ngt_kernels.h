@@ -217,6 +217,31 @@ struct QgBuildArgs {
   uint64_t code_stride;          // (id_stride / 16) * 8 * Me
 };
 
+// NGTQG encoder: per object and subspace, the nearest local centroid of the
+// residual (object - global centroid), ties to the lower local id.
+struct QgEncodeArgs {
+  const uint8_t* rows;           // padded float rows, row_bytes apart
+  uint64_t row_bytes;
+  uint64_t row0, nrows;          // encode rows [row0, row0 + nrows)
+  const float* global;           // [D]
+  const float* local;            // [M][16][dsub]
+  uint32_t M, dsub;
+  uint8_t* codes;                // [row0 + nrows][M] localID - 1
+};
+
+// Local codebook training (one workgroup per subspace): Lloyd iterations
+// over the residual subvectors of objects 1..nsample from the first 16.
+struct QgTrainArgs {
+  const uint8_t* rows;
+  uint64_t row_bytes;
+  uint32_t nsample;              // objects 1..nsample (<= 4096)
+  const float* global;
+  uint32_t M, dsub;              // dsub <= 16
+  uint32_t max_iter;
+  float* local;                  // [M][16][dsub] out
+  uint32_t* iters;               // [M] iterations run (out)
+};
+
 struct QgAdcArgs {
   const uint32_t* qids;
   uint32_t id_stride;
@@ -281,6 +306,8 @@ struct QgSearchArgs {
 hipError_t launch_qg_lut(const QgLutArgs& a, hipStream_t s);
 hipError_t launch_qg_build(const QgBuildArgs& a, hipStream_t s);
 hipError_t launch_qg_adc(const QgAdcArgs& a, hipStream_t s);
+hipError_t launch_qg_encode(const QgEncodeArgs& a, hipStream_t s);
+hipError_t launch_qg_train(const QgTrainArgs& a, hipStream_t s);
 size_t qg_search_lds_bytes(const QgSearchArgs& a);
 hipError_t launch_qg_search(const QgSearchArgs& a, uint32_t slots, hipStream_t s);
 

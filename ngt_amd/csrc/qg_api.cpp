@@ -48,7 +48,70 @@ extern "C" int ngt_amd_qg_set_quantizer(ngt_amd_index* ix, const float* global, 
   q.dsub = dsub;
   q.Me = Me;
   q.ready = true;
+  q.has_codes = false;
   return 0;
+}
+
+extern "C" int ngt_amd_qg_encode(ngt_amd_index* ix, uint8_t* codes_out) {
+  if (!ix) return fail("ngt_amd_qg_encode: bad arguments");
+  if (!ix->qg.ready) return fail("ngt_amd_qg_encode: set or train the quantizer first");
+  if (ix->nrows < 2) return fail("ngt_amd_qg_encode: the index has no objects");
+  QgState& q = ix->qg;
+  if (q.dsub > 16) return fail("ngt_amd_qg_encode: subvector dimension %u > 16 is not supported", q.dsub);
+  HIP_OK(hipSetDevice(ix->device));
+  HIP_OK(q.codes.alloc((size_t)ix->nrows * q.M));
+  HIP_OK(hipMemsetAsync(q.codes.p, 0, (size_t)q.M, ix->stream));
+  QgEncodeArgs a{};
+  a.rows = ix->rows.p;
+  a.row_bytes = ix->row_bytes;
+  a.row0 = 1;
+  a.nrows = ix->nrows - 1;
+  a.global = q.global.p;
+  a.local = q.local.p;
+  a.M = q.M;
+  a.dsub = q.dsub;
+  a.codes = q.codes.p;
+  HIP_OK(launch_qg_encode(a, ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  q.has_codes = true;
+  if (codes_out) HIP_OK(hipMemcpy(codes_out, q.codes.p, (size_t)ix->nrows * q.M, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int ngt_amd_qg_train(ngt_amd_index* ix, uint32_t M, uint32_t nsample, uint32_t max_iter,
+                                float* local_out, uint32_t* iters_out) {
+  if (!ix || M == 0) return fail("ngt_amd_qg_train: bad arguments");
+  if (ix->dim % M) return fail("ngt_amd_qg_train: dimension %u is not a multiple of M = %u", ix->dim, M);
+  const uint32_t dsub = ix->dim / M;
+  if (dsub > 16) return fail("ngt_amd_qg_train: subvector dimension %u > 16 is not supported", dsub);
+  if (nsample < 16 || nsample > 4096) return fail("ngt_amd_qg_train: nsample %u not in [16, 4096]", nsample);
+  if (ix->nrows < (uint64_t)nsample + 1) return fail("ngt_amd_qg_train: %u samples need %u objects", nsample, nsample);
+  if ((size_t)nsample * dsub + 16 * dsub + nsample + nsample / 4 + 1 > 16384)
+    return fail("ngt_amd_qg_train: nsample x dsub too large for one workgroup's LDS");
+  HIP_OK(hipSetDevice(ix->device));
+  std::vector<float> zero(ix->dim, 0.0f);
+  DevBuf<float> g, local;
+  DevBuf<uint32_t> iters;
+  HIP_OK(g.upload(zero.data(), zero.size()));
+  HIP_OK(local.alloc((size_t)M * 16 * dsub));
+  HIP_OK(iters.alloc(M));
+  QgTrainArgs a{};
+  a.rows = ix->rows.p;
+  a.row_bytes = ix->row_bytes;
+  a.nsample = nsample;
+  a.global = g.p;
+  a.M = M;
+  a.dsub = dsub;
+  a.max_iter = max_iter == 0 ? 20 : max_iter;
+  a.local = local.p;
+  a.iters = iters.p;
+  HIP_OK(launch_qg_train(a, ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  std::vector<float> h((size_t)M * 16 * dsub);
+  HIP_OK(hipMemcpy(h.data(), local.p, h.size() * sizeof(float), hipMemcpyDeviceToHost));
+  if (iters_out) HIP_OK(hipMemcpy(iters_out, iters.p, (size_t)M * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (local_out) std::copy(h.begin(), h.end(), local_out);
+  return ngt_amd_qg_set_quantizer(ix, zero.data(), h.data(), M, dsub);
 }
 
 static int alloc_qg_graph(ngt_amd_index* ix, uint64_t maxdeg) {
@@ -64,20 +127,21 @@ static int alloc_qg_graph(ngt_amd_index* ix, uint64_t maxdeg) {
 }
 
 extern "C" int ngt_amd_qg_build_graph(ngt_amd_index* ix, const uint8_t* local_codes, uint32_t max_edges) {
-  if (!ix || !local_codes || max_edges == 0) return fail("ngt_amd_qg_build_graph: bad arguments");
+  if (!ix || max_edges == 0) return fail("ngt_amd_qg_build_graph: bad arguments");
+  if (!local_codes && !ix->qg.has_codes) return fail("ngt_amd_qg_build_graph: no codes given and none encoded");
   if (!ix->qg.ready) return fail("ngt_amd_qg_build_graph: set the quantizer first");
   if (!ix->has_graph) return fail("ngt_amd_qg_build_graph: the index has no graph");
   HIP_OK(hipSetDevice(ix->device));
   QgState& q = ix->qg;
   if (alloc_qg_graph(ix, std::min<uint64_t>(ix->max_degree, max_edges))) return -1;
   DevBuf<uint8_t> codes;
-  HIP_OK(codes.upload(local_codes, (size_t)ix->nrows * q.M));
+  if (local_codes) HIP_OK(codes.upload(local_codes, (size_t)ix->nrows * q.M));
   QgBuildArgs a{};
   a.edge_off = ix->edge_off.p;
   a.edges = ix->edges.p;
   a.nrows = (uint32_t)ix->nrows;
   a.max_edges = max_edges;
-  a.local_codes = codes.p;
+  a.local_codes = local_codes ? codes.p : q.codes.p;
   a.M = q.M;
   a.Me = q.Me;
   a.qids = q.qids.p;

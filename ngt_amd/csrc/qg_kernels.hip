@@ -124,7 +124,139 @@ __global__ void __launch_bounds__(256) ngt_qg_build_kernel(QgBuildArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// ADC building blocks.
+// Encoder (the local half of Quantizer::insert, lib/NGT/NGTQ/Quantizer.h:
+// 1895-1959): residual subvector r = object - global centroid, computed in
+// double and stored as float (GenerateResidualObjectFloat, :1407-1435), coded
+// as the local centroid nearest to r.  The reference finds it with an NGT
+// insertion search of the 16-object local codebook index (createIndex with
+// range FLT_MAX, :1678-1719, Index.cpp:1260-1345), whose distances are
+// PrimitiveComparator::compareL2 over the zero-padded subvector and whose
+// results are ordered by (distance, id): the scalar restatement below keeps
+// the 16 AVX-512 lanes, their 16->8->4 fold and the double sqrt, and ties go
+// to the lower local id.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float l2_sub(const float* r, const float* c, uint32_t n) {
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) acc[j] = 0.0f;
+  for (uint32_t i = 0; i < n; i += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const float v = i + j < n ? r[i + j] - c[i + j] : 0.0f;
+      acc[j] = __builtin_fmaf(v, v, acc[j]);
+    }
+  }
+  float t4[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) t4[j] = (acc[j + 12] + acc[j + 4]) + (acc[j + 8] + acc[j]);
+  return (float)sqrt((double)((t4[0] + t4[1]) + (t4[2] + t4[3])));
+}
+
+__global__ void __launch_bounds__(256) ngt_qg_encode_kernel(QgEncodeArgs a) {
+  const uint64_t total = a.nrows * a.M;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const uint64_t o = a.row0 + t / a.M;
+    const uint32_t m = (uint32_t)(t % a.M);
+    const float* x = reinterpret_cast<const float*>(a.rows + o * a.row_bytes) + (uint64_t)m * a.dsub;
+    const float* g = a.global + (uint64_t)m * a.dsub;
+    float r[16];
+    uint32_t best = 0;
+    float bd = 0.0f;
+    if (a.dsub <= 16) {
+#pragma unroll
+      for (int d = 0; d < 16; d++) r[d] = (uint32_t)d < a.dsub ? (float)((double)x[d] - (double)g[d]) : 0.0f;
+      for (uint32_t c = 0; c < 16; c++) {
+        const float dc = l2_sub(r, a.local + ((uint64_t)m * 16 + c) * a.dsub, a.dsub);
+        if (c == 0 || dc < bd) { bd = dc; best = c; }
+      }
+    }
+    a.codes[o * a.M + m] = (uint8_t)best;
+  }
+}
+
+// Local codebook training, one 256-thread workgroup per subspace: the sample
+// is the residual subvectors of objects 1..nsample (the reference's dynamic
+// k-means collects the first localCentroidLimit * localClusteringSampleCoefficient
+// = 16 * 100 objects, Quantizer.h:1803-1844), the initial centroids are its
+// first 16 (Clustering::InitializationModeHead, Clustering.h:835-843), then
+// Lloyd iterations with exact nearest-centroid assignment (l2_sub, ties to the
+// lower id) and centroids as float means summed in sample order, until no
+// centroid changes or max_iter.  An empty cluster takes the sample farthest
+// from its centroid among clusters with >= 2 members (the intent of
+// moveFartherObjectsToEmptyClusters, :405-437).  NOT the reference's
+// kmeansWithNGT: its assignment is an approximate NGT range search per
+// centroid (assignWithNGT, :440-577), so codebooks differ; encoding, LUT,
+// ADC and search given a codebook are the pinned parts.
+__global__ void __launch_bounds__(256) ngt_qg_train_kernel(QgTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t m = blockIdx.x;
+  const uint32_t ds = a.dsub, n = a.nsample;
+  float* s = reinterpret_cast<float*>(smem);         // [n][ds]
+  float* cen = s + (uint64_t)n * ds;                  // [16][ds]
+  float* sd = cen + 16 * ds;                          // [n] distance to own centroid
+  uint8_t* asg = reinterpret_cast<uint8_t*>(sd + n);  // [n]
+  __shared__ uint32_t cnt[16];
+  __shared__ int changed;
+  for (uint32_t i = threadIdx.x; i < n * ds; i += blockDim.x) {
+    const uint32_t o = i / ds + 1, d = i % ds;
+    const float* x = reinterpret_cast<const float*>(a.rows + (uint64_t)o * a.row_bytes);
+    s[i] = (float)((double)x[m * ds + d] - (double)a.global[m * ds + d]);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 16 * ds; i += blockDim.x) cen[i] = s[i];
+  __syncthreads();
+  uint32_t it = 0;
+  for (; it < a.max_iter; it++) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      float r[16];
+      for (uint32_t d = 0; d < 16; d++) r[d] = d < ds ? s[i * ds + d] : 0.0f;
+      uint32_t best = 0;
+      float bd = 0.0f;
+      for (uint32_t c = 0; c < 16; c++) {
+        const float dc = l2_sub(r, cen + c * ds, ds);
+        if (c == 0 || dc < bd) { bd = dc; best = c; }
+      }
+      asg[i] = (uint8_t)best;
+      sd[i] = bd;
+    }
+    if (threadIdx.x < 16) cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (uint32_t i = 0; i < n; i++) cnt[asg[i]]++;
+      for (uint32_t c = 0; c < 16; c++) {
+        if (cnt[c] != 0) continue;
+        // farthest member of any cluster with >= 2 members moves to c
+        float mx = -1.0f;
+        uint32_t mi = 0xffffffffu;
+        for (uint32_t i = 0; i < n; i++)
+          if (cnt[asg[i]] >= 2 && sd[i] > mx) { mx = sd[i]; mi = i; }
+        if (mi == 0xffffffffu) break;
+        cnt[asg[mi]]--;
+        asg[mi] = (uint8_t)c;
+        sd[mi] = 0.0f;
+        cnt[c] = 1;
+      }
+    }
+    __syncthreads();
+    // new centroids: float sums in sample order, then / count
+    if (threadIdx.x < 16 * ds) {
+      const uint32_t c = threadIdx.x / ds, d = threadIdx.x % ds;
+      float sum = 0.0f;
+      for (uint32_t i = 0; i < n; i++)
+        if (asg[i] == c) sum += s[i * ds + d];
+      const float v = cnt[c] ? sum / (float)cnt[c] : cen[c * ds + d];
+      if (__float_as_uint(v) != __float_as_uint(cen[c * ds + d])) atomicOr(&changed, 1);
+      cen[c * ds + d] = v;
+    }
+    __syncthreads();
+    if (!changed) { it++; break; }
+  }
+  for (uint32_t i = threadIdx.x; i < 16 * ds; i += blockDim.x) a.local[(uint64_t)m * 16 * ds + i] = cen[i];
+  if (threadIdx.x == 0) a.iters[m] = it;
+}
+
 // ---------------------------------------------------------------------------
 // Four table lookups into the 16-byte table t0..t3 (little-endian dwords):
 // byte b of the result = table[nibble of byte b of `w` at bit `sh`] for
@@ -724,6 +856,23 @@ hipError_t launch_qg_build(const QgBuildArgs& a, hipStream_t s) {
   uint64_t blocks = ((uint64_t)a.nrows + 3) / 4;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(ngt_qg_build_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_qg_encode(const QgEncodeArgs& a, hipStream_t s) {
+  if (a.nrows == 0) return hipSuccess;
+  if (a.dsub == 0 || a.dsub > 16) return hipErrorInvalidValue;
+  uint64_t blocks = (a.nrows * a.M + 255) / 256;
+  if (blocks > 262144) blocks = 262144;
+  hipLaunchKernelGGL(ngt_qg_encode_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_qg_train(const QgTrainArgs& a, hipStream_t s) {
+  if (a.dsub == 0 || a.dsub > 16 || a.nsample < 16) return hipErrorInvalidValue;
+  const size_t lds = ((size_t)a.nsample * a.dsub + 16 * a.dsub + a.nsample) * sizeof(float) + a.nsample;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ngt_qg_train_kernel, dim3(a.M), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 

@@ -209,10 +209,36 @@ class DeviceIndex(object):
         self.qg_M = M
         self.qg_Me = (M + 1) // 2 * 2
 
-    def qg_build_graph(self, local_codes, max_edges=128):
-        """local_codes: [nrows, M] localID - 1 (0..15) of every object."""
+    def qg_build_graph(self, local_codes=None, max_edges=128):
+        """local_codes: [nrows, M] localID - 1 (0..15) of every object, or
+        None for the codes of the last qg_encode (kept in HBM)."""
+        if local_codes is None:
+            _chk(self.L.ngt_amd_qg_build_graph(self.h, None, max_edges))
+            return
         c = np.ascontiguousarray(local_codes, dtype=np.uint8)
         _chk(self.L.ngt_amd_qg_build_graph(self.h, c.ctypes.data, max_edges))
+
+    def qg_encode(self, return_codes=True):
+        """Nearest local centroid of every object's residual subvectors (the
+        encoder of Quantizer::insert); codes stay on the device for
+        qg_build_graph(None).  Returns [nrows, M] localID - 1, or None."""
+        if not return_codes:
+            _chk(self.L.ngt_amd_qg_encode(self.h, None))
+            return None
+        out = np.zeros((self.nrows, self.qg_M), np.uint8)
+        _chk(self.L.ngt_amd_qg_encode(self.h, out.ctypes.data))
+        return out
+
+    def qg_train(self, M, nsample=1600, max_iter=20):
+        """Train and install NGTQG local codebooks (global = zero vector) from
+        objects 1..nsample.  Returns (local [M, 16, dim/M], iterations [M])."""
+        dsub = self.dim // M
+        loc = np.zeros((M, 16, dsub), np.float32)
+        its = np.zeros(M, np.uint32)
+        _chk(self.L.ngt_amd_qg_train(self.h, M, nsample, max_iter, loc.ctypes.data, its.ctypes.data))
+        self.qg_M = M
+        self.qg_Me = (M + 1) // 2 * 2
+        return loc, its
 
     def qg_set_graph(self, qoff, qids, code_off, codes):
         qoff = np.ascontiguousarray(qoff, dtype=np.uint64)

@@ -207,3 +207,90 @@ def test_ngtqg_capi_matches_reference(tmp_path, with_grp):
             n = int(z["n_" + key][qi])
             assert int(bn[qi]) == n and list(bi[qi, :n]) == list(z["ids_" + key][qi][:n]), (key, qi)
     ix.close()
+
+
+# ---------------------------------------------------------------------------
+# encoder and codebook training (ngt_amd_qg_encode / ngt_amd_qg_train)
+# ---------------------------------------------------------------------------
+def _l2_sub(r, c):
+    """compareL2 of zero-padded subvectors (dsub <= 16), as l2_sub in
+    qg_kernels.hip: 16 float lanes, 16->8->4 fold, sqrt in double."""
+    diff = (r - c).astype(np.float32)
+    v = np.zeros(diff.shape[:-1] + (16,), np.float32)
+    v[..., :diff.shape[-1]] = diff
+    acc = (v * v).astype(np.float32)
+    t4 = (acc[..., 12:16] + acc[..., 4:8]) + (acc[..., 8:12] + acc[..., 0:4])
+    s = (t4[..., 0] + t4[..., 1]) + (t4[..., 2] + t4[..., 3])
+    return np.sqrt(s.astype(np.float64)).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_qg_encoder_matches_reference_ivt(name):
+    """Every object of the reference-quantized index coded with the
+    reference's own codebooks: the device encoder's local ids equal qg/ivt's
+    (the reference's insertion search over each 16-centroid codebook index)."""
+    qg, rows, valid, *_ = state(name)
+    ix = device_qg(name)
+    codes = ix.qg_encode()
+    ref = local_codes(qg, rows.shape[0])
+    have = np.zeros(rows.shape[0], bool)
+    have[:min(rows.shape[0], qg["local_ids"].shape[0])] = qg["local_ids"][:rows.shape[0]].min(1) > 0
+    have[0] = False
+    bad = np.argwhere((codes != ref) & have[:, None])
+    assert have.sum() > 0.9 * (rows.shape[0] - 1)
+    assert len(bad) == 0, ("mismatches", len(bad), bad[:5].tolist())
+    # the codes kept in HBM build the same quantized graph as the ivt codes
+    ids_ref, codes_ref = ix.qg_get_graph()
+    ix.qg_build_graph(None, CASES[name][2])
+    ids_enc, codes_enc = ix.qg_get_graph()
+    assert np.array_equal(ids_ref, ids_enc) and np.array_equal(codes_ref, codes_enc)
+    ix.close()
+
+
+def test_qg_train_fixpoint_and_search():
+    """Trained codebooks (global = 0, dsub = 1, 1600 samples): every subspace
+    that converged is a Lloyd fixpoint -- each centroid is the float mean, in
+    sample order, of the samples nearest to it -- and the quantized graph built
+    from the device-encoded codes finds the exact neighbours at recall >= 0.9
+    (C1 data, k=10, expansion 3)."""
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("c1_qg")
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows, valid)
+    ix.set_graph(offs, ids)
+    ix.set_tree(tree)
+    ix.set_search_property(int(prop["EdgeSizeForSearch"]), int(prop["DynamicEdgeSizeBase"]),
+                           int(prop["DynamicEdgeSizeRate"]), int(prop["SeedSize"]), 0)
+    loc, its = ix.qg_train(dim, nsample=1600, max_iter=20)
+    assert loc.shape == (dim, 16, 1) and its.max() <= 20
+    s = rows[1:1601, :dim].astype(np.float32)
+    checked = 0
+    for m in range(dim):
+        if its[m] >= 20:
+            continue
+        c = loc[m]                                             # [16, 1]
+        d = _l2_sub(s[:, m:m + 1][:, None, :], c[None, :, :])  # [1600, 16]
+        a = d.argmin(1)                                        # ties -> lower id
+        cnt = np.bincount(a, minlength=16)
+        if cnt.min() == 0:
+            continue
+        for ci in range(16):
+            mem = s[a == ci, m]
+            mean = np.float32(np.cumsum(mem, dtype=np.float32)[-1]) / np.float32(len(mem))
+            assert np.float32(mean).view(np.uint32) == np.float32(c[ci, 0]).view(np.uint32), (m, ci)
+        checked += 1
+    assert checked > dim // 2
+    codes = ix.qg_encode()
+    assert codes.max() <= 15
+    d = _l2_sub(rows[1:, :dim, None, None], loc[None, :, :, :])  # [n, dim, 16]
+    assert np.array_equal(codes[1:], d.argmin(2).astype(np.uint8))
+    ix.qg_build_graph(None, maxe)
+    qs = queries_c1()[:100]
+    gi, gd, gn, _ = ix.qg_search(qs, k=10, epsilon=0.1, result_expansion=3.0, seed_mode=SEED_TREE)
+    li, ld, ln = ix.linear_search(qs, k=10)
+    rec = np.mean([len(set(gi[i, :10]) & set(li[i, :ln[i]])) / 10.0 for i in range(len(qs))])
+    assert rec >= 0.9, rec
+    ix.close()
+
+
+def queries_c1():
+    return np.load(os.path.join(GOLD, "queries.npy")).astype(np.float32)
