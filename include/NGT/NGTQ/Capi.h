@@ -7,9 +7,14 @@
  * Same names, argument types, defaults (ngtqg_initialize_query: size 20,
  * epsilon 0.03, result_expansion 3.0, radius FLT_MAX) and error convention
  * ("Capi : <func>() : Error: <what>" / "... parametor error: ...") as the
- * reference.  ngtqg_quantize (codebook training + encoding, SURVEY.md 8(f)
- * row 3) reports an error in this build: indexes are quantized by the
- * reference's `ngtqg quantize` and opened here.
+ * reference.  ngtqg_quantize (NGTQ/Capi.cpp:120-131 -> NGTQG::Index::quantize,
+ * QuantizedGraph.h:456-475) trains the local codebooks, encodes every object
+ * and builds the quantized graph on the device, and writes <index>/qg in the
+ * reference's formats (qg/prf and the codebook prf files byte-identical to
+ * the reference's; codebook indexes built by this library's ANNG
+ * construction).  Its k-means is Lloyd's with exact assignment, not the
+ * reference's kmeansWithNGT, so codebooks differ from the reference's own;
+ * given a codebook, codes and quantized graph are the reference's.
  *
  * Extension (not in the reference): ngtqg_batch_search_index.
  */

@@ -2,6 +2,7 @@
 // See index_io.h for the format citations.
 #include "index_io.h"
 
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -146,8 +147,24 @@ void HostProperty::to_kv() {
     os << epsilon_for_creation;
     kv["EpsilonForCreation"] = os.str();
   }
-  kv["PrefetchOffset"] = std::to_string(prefetch_offset);
-  kv["PrefetchSize"] = std::to_string(prefetch_size);
+  // 0 = the object space's runtime values, which save() exports
+  // (ObjectSpace::setPrefetchOffset/Size, lib/NGT/ObjectSpace.h:268-283)
+  const int pdim = ((dimension - 1) / 16 + 1) * 16;
+  kv["PrefetchOffset"] = std::to_string(prefetch_offset ? prefetch_offset
+                                                        : (int)floor(300.0 / ((float)pdim + 30.0) + 1.0));
+  kv["PrefetchSize"] = std::to_string(prefetch_size ? prefetch_size : dimension * (object_type == 1 ? 1 : 4));
+  // keys a fresh NGT::Property writes (Index.h:60-75, 150-170; Graph.h:386-402, 430-450)
+  static const char* kMore[][2] = {{"AccuracyTable", ""},
+                                   {"BuildTimeLimit", "0"},
+                                   {"EdgeSizeLimitForCreation", "5"},
+                                   {"IncomingEdge", "80"},
+                                   {"IncrimentalEdgeSizeLimitForTruncation", "0"},
+                                   {"OutgoingEdge", "10"},
+                                   {"PathAdjustmentInterval", "0"},
+                                   {"ThreadPoolSize", "32"},
+                                   {"TruncationThreadPoolSize", "8"}};
+  for (auto& m : kMore)
+    if (!kv.count(m[0])) kv[m[0]] = m[1];
 }
 
 void HostIndex::init_layout() {

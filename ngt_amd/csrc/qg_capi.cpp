@@ -7,6 +7,10 @@
 // Search = NGTQG::Index::search(SearchQuery&) (:354-372) as one device batch.
 #include <float.h>
 #include <stdlib.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <fstream>
 
 #include <iostream>
 #include <sstream>
@@ -88,6 +92,96 @@ std::string run(QgCapiIndex* ix, const float* queries, uint32_t nq, size_t size,
   return "";
 }
 
+// One NGT index (a codebook) of `n` float rows of `d` dimensions: created,
+// built and saved through this library's ngt_* API (obj/prf/grp/tre).
+std::string write_codebook(const std::string& dir, const float* rows, uint32_t n, uint32_t d, int edge_create,
+                           int edge_search) {
+  NGTError er = ngt_create_error_object();
+  NGTProperty prop = ngt_create_property(er);
+  std::string e;
+  NGTIndex cb = NULL;
+  if (!ngt_set_property_dimension(prop, (int32_t)d, er) || !ngt_set_property_object_type_float(prop, er) ||
+      !ngt_set_property_distance_type_l2(prop, er) ||
+      !ngt_set_property_edge_size_for_creation(prop, (int16_t)edge_create, er) ||
+      !ngt_set_property_edge_size_for_search(prop, (int16_t)edge_search, er))
+    e = ngt_get_error_string(er);
+  if (e.empty() && !(cb = ngt_create_graph_and_tree(dir.c_str(), prop, er))) e = ngt_get_error_string(er);
+  for (uint32_t i = 0; e.empty() && i < n; i++)
+    if (ngt_insert_index_as_float(cb, const_cast<float*>(rows + (size_t)i * d), d, er) == 0)
+      e = ngt_get_error_string(er);
+  if (e.empty() && !ngt_create_index(cb, 16, er)) e = ngt_get_error_string(er);
+  if (e.empty() && !ngt_save_index(cb, dir.c_str(), er)) e = ngt_get_error_string(er);
+  if (cb) ngt_close_index(cb);
+  ngt_destroy_property(prop);
+  ngt_destroy_error_object(er);
+  return e;
+}
+
+std::string write_quantizer(const std::string& qd, const ngt_amd::HostIndex& h, uint32_t dim, uint32_t M,
+                            uint32_t dsub, const std::vector<float>& local, const std::vector<uint8_t>& codes,
+                            uint32_t stride, uint64_t cstride, const std::vector<uint32_t>& qids,
+                            const std::vector<uint8_t>& qcodes) {
+  if (mkdir(qd.c_str(), 0755) != 0) return "cannot create " + qd;
+  {
+    // NGTQ::Property::save (lib/NGT/NGTQ/Quantizer.h:218-240), the frame of
+    // constructQuantizedGraphFrame (QuantizedGraph.h:423-454)
+    std::ofstream f(qd + "/prf");
+    f << "BatchSize\t1000\nCentroidCreationMode\t1\nDataSize\t" << (uint64_t)dim * 4 << "\nDataType\t1\n"
+      << "Dimension\t" << dim << "\nDistanceType\t2\nGlobalCentroidLimit\t1\nGlobalRange\t0\n"
+      << "LocalCentroidCreationMode\t2\nLocalCentroidLimit\t16\nLocalCodebookState\t1\n"
+      << "LocalDivisionNo\t" << M << "\nLocalIDByteSize\t2\nLocalRange\t0\nLocalSampleCoefficient\t100\n"
+      << "SingleLocalCodebook\t0\nThreadSize\t24\n";
+    if (!f) return "cannot write " + qd + "/prf";
+  }
+  // global codebook: the zero vector (QuantizedGraph.h:397-399), edge sizes 10 / 40
+  std::vector<float> zero(dim, 0.0f);
+  std::string e = write_codebook(qd + "/global", zero.data(), 1, dim, 10, 40);
+  if (!e.empty()) return e;
+  for (uint32_t m = 0; m < M && e.empty(); m++)
+    e = write_codebook(qd + "/local-" + std::to_string(m), local.data() + (size_t)m * 16 * dsub, 16, dsub, 10, 40);
+  if (!e.empty()) return e;
+  {
+    // ivt: every valid object under global centroid 1, local ids 1..16 padded to 4 B
+    std::ofstream f(qd + "/ivt", std::ios::binary);
+    const uint64_t n = 2;
+    f.write(reinterpret_cast<const char*>(&n), 8);
+    f.put('-');
+    f.put('+');
+    uint32_t cnt = 0;
+    for (uint64_t i = 1; i < h.nrows; i++) cnt += h.valid[i] ? 1 : 0;
+    const uint16_t nids = (uint16_t)M;
+    f.write(reinterpret_cast<const char*>(&cnt), 4);
+    f.write(reinterpret_cast<const char*>(&nids), 2);
+    const size_t pad = ((size_t)(nids * 2 - 1) / 4 + 1) * 4;
+    std::vector<uint16_t> lid(pad / 2, 0);
+    for (uint64_t i = 1; i < h.nrows; i++) {
+      if (!h.valid[i]) continue;
+      const uint32_t id = (uint32_t)i;
+      for (uint32_t m = 0; m < M; m++) lid[m] = (uint16_t)(codes[i * M + m] + 1);
+      f.write(reinterpret_cast<const char*>(&id), 4);
+      f.write(reinterpret_cast<const char*>(lid.data()), pad);
+    }
+    if (!f) return "cannot write " + qd + "/ivt";
+  }
+  if (stride) {
+    std::ofstream f(qd + "/grp", std::ios::binary);
+    const uint64_t hdr[2] = {M, h.nrows};
+    f.write(reinterpret_cast<const char*>(hdr), 16);
+    const uint64_t me = (M + 1) / 2 * 2;
+    for (uint64_t v = 0; v < h.nrows; v++) {
+      const uint32_t* r = qids.data() + v * stride;
+      uint32_t deg = 0;
+      while (deg < stride && r[deg] != 0) deg++;
+      f.write(reinterpret_cast<const char*>(&deg), 4);
+      f.write(reinterpret_cast<const char*>(r), (size_t)deg * 4);
+      const uint64_t nb = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+      f.write(reinterpret_cast<const char*>(qcodes.data() + v * cstride), (std::streamsize)(nb * 8 * me));
+    }
+    if (!f) return "cannot write " + qd + "/grp";
+  }
+  return "";
+}
+
 }  // namespace
 
 extern "C" {
@@ -126,13 +220,69 @@ void ngtqg_close_index(NGTQGIndex index) {
   delete static_cast<QgCapiIndex*>(index);
 }
 
+// NGTQG::Index::quantize (lib/NGT/NGTQ/QuantizedGraph.h:456-475) on the device:
+// nothing when <index>/qg exists; else the quantizer frame (:423-454), the
+// codebooks, every object's local codes (:392-421) and the quantized graph
+// (:387-390), written in the reference's file formats: qg/prf (NGTQ::Property),
+// qg/global and qg/local-<m> as NGT indexes (built by this library's ANNG
+// construction), qg/ivt (Repository<InvertedIndexEntry<uint16_t>>) and qg/grp
+// (QuantizedGraphRepository::serialize, :117-128).  The local codebooks come
+// from ngt_amd_qg_train (Lloyd), not the reference's kmeansWithNGT.
 bool ngtqg_quantize(const char* indexPath, NGTQGQuantizationParameters parameters, NGTError error) {
-  (void)indexPath;
-  (void)parameters;
-  report(error, std::string("Capi : ") + __FUNCTION__ +
-                    "() : Error: quantization (codebook training) is not available in this build; "
-                    "quantize with the reference's `ngtqg quantize` and open the index here");
-  return false;
+  auto err = [&](const std::string& e) {
+    report(error, std::string("Capi : ") + __FUNCTION__ + "() : Error: " + e);
+    return false;
+  };
+  if (!indexPath) return err("null index path");
+  const std::string qd = std::string(indexPath) + "/qg";
+  struct stat st;
+  if (stat(qd.c_str(), &st) == 0) return true;
+  ngt_amd::HostIndex h;
+  std::string e = ngt_amd::load_index(indexPath, h);
+  if (!e.empty()) return err(e);
+  if (h.prop.distance_type != NGT_AMD_DISTANCE_L2 || h.prop.object_type != NGT_AMD_OBJECT_FLOAT)
+    return err("NGTQG supports L2 float indexes only");
+  const uint32_t dim = (uint32_t)h.prop.dimension;
+  // NGTQG::Index::getNumberOfSubvectors (:374-385)
+  size_t dsub = (size_t)parameters.dimension_of_subvector;
+  if (dsub == 0) {
+    dsub = dim > 400 ? 2 : 1;
+    dsub = dim % dsub == 0 ? dsub : 1;
+  }
+  if (dim % dsub != 0) return err("dimensionOfSubvector is invalid. " + std::to_string(dim) + " : " +
+                                  std::to_string(dsub));
+  const uint32_t M = (uint32_t)(dim / dsub);
+  uint64_t nvalid = 0;
+  for (uint64_t i = 1; i < h.nrows; i++) nvalid += h.valid[i] ? 1 : 0;
+  if (nvalid < 16) return err("at least 16 objects are needed to train 16 centroids per subspace");
+  QgCapiIndex ix;
+  int dev = 0;
+  if (const char* env = getenv("NGT_AMD_DEVICE")) dev = atoi(env);
+  if (ngt_amd_index_create(&ix.dev, dev, h.prop.distance_type, h.prop.object_type, dim)) return err(amd_err());
+  if (ngt_amd_index_set_objects(ix.dev, h.rows.data(), h.nrows, h.valid.data())) return err(amd_err());
+  // the dynamic k-means samples the first localCentroidLimit * LocalSampleCoefficient objects
+  const uint32_t nsample = (uint32_t)std::min<uint64_t>(16 * 100, h.nrows - 1);
+  std::vector<float> local((size_t)M * 16 * dsub);
+  if (ngt_amd_qg_train(ix.dev, M, nsample, 20, local.data(), nullptr)) return err(amd_err());
+  std::vector<uint8_t> codes((size_t)h.nrows * M);
+  if (ngt_amd_qg_encode(ix.dev, codes.data())) return err(amd_err());
+  const uint32_t max_edges = (uint32_t)parameters.max_number_of_edges;
+  std::vector<uint32_t> qids;
+  std::vector<uint8_t> qcodes;
+  uint32_t stride = 0;
+  uint64_t cstride = 0;
+  if (max_edges != 0) {
+    if (ngt_amd_index_set_graph(ix.dev, h.edge_off.data(), h.edges.data(), h.edges.size())) return err(amd_err());
+    if (ngt_amd_qg_build_graph(ix.dev, nullptr, max_edges)) return err(amd_err());
+    stride = ngt_amd_qg_max_degree(ix.dev);
+    cstride = ngt_amd_qg_code_stride(ix.dev);
+    qids.resize((size_t)h.nrows * stride);
+    qcodes.resize((size_t)h.nrows * cstride);
+    if (ngt_amd_qg_get_graph(ix.dev, qids.data(), qcodes.data())) return err(amd_err());
+  }
+  e = write_quantizer(qd, h, dim, M, (uint32_t)dsub, local, codes, stride, cstride, qids, qcodes);
+  if (!e.empty()) return err(e);
+  return true;
 }
 
 bool ngtqg_search_index(NGTQGIndex index, NGTQGQuery query, NGTObjectDistances results, NGTError error) {

@@ -12,6 +12,23 @@ from . import NativeError, lib
 from ._sigs import NGTQGQuery, NGTQGQuantizationParameters
 
 
+def quantize(path, dimension_of_subvector=0, max_number_of_edges=128):
+    """``ngtqg quantize`` / ngtqg_quantize (NGTQ/Capi.cpp:120-131): writes
+    <path>/qg (codebooks, codes, quantized graph) on the device; a no-op when
+    <path>/qg exists (QuantizedGraph.h:456-475)."""
+    L = lib()
+    err = L.ngt_create_error_object()
+    try:
+        p = NGTQGQuantizationParameters()
+        L.ngtqg_initialize_quantization_parameters(ctypes.byref(p))
+        p.dimension_of_subvector = float(dimension_of_subvector)
+        p.max_number_of_edges = int(max_number_of_edges)
+        if not L.ngtqg_quantize(path.encode(), p, err):
+            raise NativeError(L.ngt_get_error_string(err).decode())
+    finally:
+        L.ngt_destroy_error_object(err)
+
+
 class QuantizedIndex(object):
     def __init__(self, path, max_no_of_edges=128, zero_based_numbering=True, tree_disabled=False,
                  log_disabled=False):

@@ -294,3 +294,49 @@ def test_qg_train_fixpoint_and_search():
 
 def queries_c1():
     return np.load(os.path.join(GOLD, "queries.npy")).astype(np.float32)
+
+
+def test_ngtqg_quantize_capi(tmp_path):
+    """ngtqg_quantize on the C1 ONNG: the qg/ directory is written in the
+    reference's formats -- qg/prf and qg/global/prf byte-identical to the
+    reference's, every codebook a complete NGT index (prf/obj/grp/tre), qg/ivt
+    holding the device encoder's codes for the codebooks written, qg/grp the
+    quantized graph built from them -- ngtqg_open_index reads it back, search
+    reaches recall >= 0.9, and a second call leaves it alone."""
+    import hashlib
+    from ngt_amd.qg import QuantizedIndex, quantize
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("c1_qg")
+    d = tmp_path / "idx"
+    d.mkdir()
+    for f in ["prf", "obj", "grp", "tre"]:
+        os.symlink(os.path.join(GOLD, "c1_onng", f), str(d / f))
+    quantize(str(d), 0, 128)
+    q = str(d / "qg")
+    for f in ["prf", os.path.join("global", "prf")]:
+        assert open(os.path.join(q, f), "rb").read() == open(os.path.join(GOLD, "c1_qg", "qg", f), "rb").read(), f
+    for sub in ["global", "local-0", "local-127"]:
+        assert sorted(os.listdir(os.path.join(q, sub))) == ["grp", "obj", "prf", "tre"], sub
+    mine = F.read_qg(str(d), offs, ids, 128)
+    # the codes in ivt are the encoder's for the written codebooks
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows, valid)
+    ix.qg_set_quantizer(mine["global"], mine["local"][:, 1:17, :])
+    codes = ix.qg_encode()
+    assert np.array_equal(codes[1:], (mine["local_ids"][1:rows.shape[0]].astype(np.int32) - 1).astype(np.uint8))
+    ix.close()
+    # qg/grp: the quantized graph of those codes (same bytes as read_qg constructs)
+    raw = open(os.path.join(q, "grp"), "rb").read()
+    assert raw == F.serialize_qg_grp(mine)
+    h0 = hashlib.sha256(open(os.path.join(q, "ivt"), "rb").read()).hexdigest()
+    quantize(str(d), 0, 128)  # exists: nothing happens
+    assert hashlib.sha256(open(os.path.join(q, "ivt"), "rb").read()).hexdigest() == h0
+    qi = QuantizedIndex(str(d))
+    qs = queries_c1()[:100]
+    bi, bd, bn = qi.batch_search(qs, size=10, epsilon=0.1, result_expansion=3.0)
+    lx = DeviceIndex("l2", "float", dim)
+    lx.set_objects(rows, valid)
+    li, ld, ln = lx.linear_search(qs, k=10)
+    lx.close()
+    rec = np.mean([len(set(bi[i, :bn[i]].tolist()) & set(li[i, :ln[i]].tolist())) / 10.0 for i in range(len(qs))])
+    assert rec >= 0.9, rec
+    qi.close()
