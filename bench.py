@@ -167,7 +167,7 @@ def recall_at(ids, gt, k):
     return hit / float(gt.shape[0] * k)
 
 
-def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.002):
+def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.0005):
     """Smallest epsilon whose mean recall@k reaches the target (ngt eval
     semantics, Optimizer.h:400): given candidates, or by doubling + bisection."""
     if eps_list:

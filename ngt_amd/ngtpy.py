@@ -1,0 +1,125 @@
+"""``ngtpy``-compatible surface over the drop-in C API (python/src/ngtpy.cpp:30-330
+for the behaviour, :505-560 for the names and defaults).
+
+Same module-level ``create`` and ``Index`` class, same argument names and
+defaults, same result shapes: a list of ``(id, distance)`` tuples, or an int32
+id array with ``with_distance=False``, ids zero-based unless
+``zero_based_numbering=False``.  Every search runs on the MI355X through
+libngt_amd.so (``ngt_batch_search_index`` / ``_using_only_graph`` /
+``ngt_batch_linear_search_index``); there is no host fallback.
+"""
+import numpy as np
+
+from . import NativeError
+from . import base
+
+FLT_MAX = 3.4028234663852886e38
+INT_MIN = -(2 ** 31)
+
+
+def create(path, dimension, edge_size_for_creation=10, edge_size_for_search=40, distance_type="L2",
+           object_type="Float"):
+    """ngtpy.create (ngtpy.cpp:52-101): an empty index directory."""
+    ot = {"Float": "Float", "float": "Float", "Byte": "Integer", "byte": "Integer"}.get(object_type)
+    if ot is None:
+        raise NativeError("ngtpy::create: invalid object type. " + object_type)
+    if distance_type not in ("L1", "L2", "Hamming", "Jaccard", "Angle", "Normalized Angle", "Cosine",
+                             "Normalized Cosine"):
+        raise NativeError("ngtpy::create: invalid distance type. " + distance_type)
+    base.Index.create(path, dimension, edge_size_for_creation, edge_size_for_search, ot, distance_type)
+
+
+class Index(object):
+    """ngtpy.Index (ngtpy.cpp:30-50): defaults k=20, epsilon=0.1,
+    radius=FLT_MAX, edge size from the property."""
+
+    def __init__(self, path, read_only=False, zero_based_numbering=True, tree_disabled=False,
+                 log_disabled=False):
+        self._ix = base.Index(path)
+        self.read_only = read_only
+        self.zero = zero_based_numbering
+        self.tree = not tree_disabled
+        self.num_of_search_objects = 20
+        self.epsilon = 0.1
+        self.radius = FLT_MAX
+        self.edge_size = -1
+        self.distance_computations = 0
+
+    def _id_out(self, ids):
+        return ids.astype(np.int64) - 1 if self.zero else ids.astype(np.int64)
+
+    def _id_in(self, oid):
+        return oid + 1 if self.zero else oid
+
+    def _results(self, ids, ds, n, with_distance):
+        ids = self._id_out(ids[0, :n[0]])
+        if not with_distance:
+            return ids.astype(np.int32)
+        return [(int(i), float(d)) for i, d in zip(ids, ds[0, :n[0]])]
+
+    def search(self, query, size=0, epsilon=-FLT_MAX, edge_size=INT_MIN, expected_accuracy=-FLT_MAX,
+               with_distance=True):
+        """ngtpy.cpp:141-214: tree-seeded search unless tree_disabled."""
+        if expected_accuracy > 0.0:
+            raise NativeError("ngtpy::search: expected_accuracy needs the optimizer's accuracy table "
+                              "(graph tooling, out of scope); pass epsilon")
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(1, -1)
+        k = size if size > 0 else self.num_of_search_objects
+        eps = self.epsilon if epsilon <= -1.0 else epsilon
+        es = self.edge_size if edge_size < -2 else edge_size
+        ids, ds, n = self._ix.batch_search(q, k, eps, self.radius, es, graph_only=not self.tree)
+        self.distance_computations += int(self._ix.last_search_counters()[0])
+        return self._results(ids, ds, n, with_distance)
+
+    def linear_search(self, query, size=0, with_distance=True):
+        """ngtpy.cpp:216-268: exact k-NN by full scan."""
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(1, -1)
+        k = size if size > 0 else self.num_of_search_objects
+        ids, ds, n = self._ix.batch_linear_search(q, k)
+        return self._results(ids, ds, n, with_distance)
+
+    def get_num_of_distance_computations(self):
+        return self.distance_computations
+
+    def set(self, num_of_search_objects=0, search_radius=-FLT_MAX, epsilon=-FLT_MAX, edge_size=INT_MIN,
+            expected_accuracy=-FLT_MAX):
+        """ngtpy.cpp:322-333: a non-positive / out-of-range value keeps the default."""
+        if num_of_search_objects > 0:
+            self.num_of_search_objects = num_of_search_objects
+        if epsilon > -1.0:
+            self.epsilon = epsilon
+        if search_radius >= 0.0:
+            self.radius = search_radius
+        if edge_size >= -2:
+            self.edge_size = edge_size
+
+    def insert(self, object, debug=False):
+        """ngtpy.cpp:119-139: append one object (no graph update until build_index)."""
+        return self._id_out(np.array([self._ix.insert_object(object)]))[0].item()
+
+    def batch_insert(self, objects, num_threads=8, debug=False):
+        """ngtpy.cpp:98-117: append all rows, then build the index on the GPU."""
+        objs = np.asarray(objects, dtype=np.float32)
+        if objs.ndim != 2 or objs.shape[1] != self._ix.dim:
+            raise NativeError("ngtpy::insert: Error! dimensions are inconsitency. %d:%d"
+                              % (self._ix.dim, objs.shape[-1]))
+        self._ix.insert(objs, num_threads)
+        self.distance_computations = 0
+
+    def build_index(self, num_threads=8, target_size_of_graph=0):
+        self._ix.build_index(num_threads)
+
+    def get_object(self, object_id):
+        return [float(x) for x in self._ix.get_object(self._id_in(object_id))]
+
+    def remove(self, object_id):
+        L = self._ix._L
+        self._ix._check(L.ngt_remove_index(self._ix.index, self._id_in(object_id), self._ix.err), self._ix.err)
+
+    def save(self):
+        if self.read_only:
+            raise NativeError("ngtpy::save: the index is read only")
+        self._ix.save()
+
+    def close(self):
+        self._ix.close()
