@@ -418,9 +418,15 @@ def main():
         log("phase cycles/query: pop %.3g ids %.3g codes+adc %.3g accept %.3g (sum %.3g)" % (
             tot[0], tot[1], tot[2], tot[3], tot.sum()))
 
-    cpu = None
-    if rank == 0 and not args.no_cpu and world == 1:
-        cpu = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric)
+    cpu = parity = None
+    if rank == 0 and not args.no_cpu and world == 1 and not shard:
+        run(chosen, 0, visited=-1 if args.mode == "exact" and args.visited == -2 else None)
+        torch.cuda.synchronize()
+        full_cnt = cnt.cpu().numpy()
+        run(chosen, 0)  # the timed configuration's own results
+        torch.cuda.synchronize()
+        gpu_out = (out_i.cpu().numpy().view(np.uint32), out_d.cpu().numpy(), out_n.cpu().numpy().view(np.uint32))
+        cpu, parity = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric, gpu_out, full_cnt)
 
     if rank == 0:
         if args.mode == "exact" and not c3:
@@ -463,6 +469,7 @@ def main():
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "parity_sample": parity,
             "sweep": sweep,
         }
         if args.mode == "qg":
@@ -498,10 +505,34 @@ def measured_traffic(mode, config, graph, eps, visited):
     return None
 
 
-def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric):
-    """The oracle restatement (scalar, 1 thread) on a bounded sample of the
-    same workload: same graph, seeds and epsilon (and quantized graph for qg),
-    queries until the budget."""
+def host_cpu():
+    """lscpu's model name and CPU count, and the threads the baseline may use
+    (the process's affinity, capped by OMP_NUM_THREADS when set)."""
+    model, ncpu = "unknown", os.cpu_count() or 1
+    try:
+        import subprocess
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+            elif line.startswith("CPU(s):"):
+                ncpu = int(line.split(":", 1)[1])
+    except (OSError, ValueError):
+        pass
+    threads = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS"):
+        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+    return model, ncpu, max(1, threads)
+
+
+def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_out, gpu_cnt):
+    """The CPU baseline and the parity sample in one: the oracle restatement
+    (oracle/ngt_oracle.c, the reference's 16-lane FMA order) built -O3 for the
+    host's widest ISA (x86-64-v4 AVX-512, else v3) with one query per thread on
+    every host core the process may use, on a bounded prefix of the same batch
+    (same graph, seeds, epsilon; for qg the same quantized graph and LUTs).
+    Its ids and float distances must equal the GPU's timed results bit for bit
+    (abort otherwise); its distance counts must equal the GPU's full-visited-set
+    counters (exact) or work counters (qg)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     t0 = time.time()
@@ -509,49 +540,75 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric):
     h_off = offsets.cpu().numpy().astype(np.uint64)
     h_edges = edges.cpu().numpy().astype(np.uint32)
     h_q = qdev.cpu().numpy()
+    model, ncpu, threads = host_cpu()
+    isa = O.host_isa()
+    L = O.native_lib(isa)
     qg = None
     if args.mode == "qg":
         ids, codes = ix.qg_get_graph()
         deg = (ids != 0).sum(1).astype(np.uint64)
         qoff = np.zeros(len(deg) + 1, np.uint64)
         qoff[1:] = np.cumsum(deg)
-        qg = {"M": args.dim, "dim": args.dim, "dsub": 1, "qoff": qoff, "qids": ids[ids != 0].astype(np.uint32),
-              "code_off": (np.arange(len(deg) + 1, dtype=np.uint64) * np.uint64(codes.shape[1])),
-              "codes": codes.reshape(-1), "global": np.zeros(args.dim, np.float32),
-              "local": None}
+        qg = {"M": args.dim, "qids": ids[ids != 0].astype(np.uint32),
+              "qoff": qoff, "code_off": (np.arange(len(deg) + 1, dtype=np.uint64) * np.uint64(codes.shape[1])),
+              "codes": np.ascontiguousarray(codes.reshape(-1))}
         lut, sc, to = ix.qg_lut(h_q[:, :args.dim])
-    log("cpu baseline: host copy %.1f s" % (time.time() - t0))
-    done = 0
-    t0 = time.perf_counter()
-    while done < h_q.shape[0] and time.perf_counter() - t0 < args.cpu_seconds:
+    log("cpu baseline: host copy %.1f s; %s, %d CPUs, %d threads, oracle %s build" % (
+        time.time() - t0, model, ncpu, threads, isa))
+
+    def run(lo, hi):
         if qg is not None:
-            oracle_qg_search(O, qg, h_rows, h_q[done], seeds[done], args.k, eps, args.expansion, lut[done],
-                             sc[done], to[done])
-        else:
-            O.search(metric, h_rows, h_off, h_edges, h_q[done], seeds[done], args.k, np.float32(eps), edge_size=0)
-        done += 1
-    el = time.perf_counter() - t0
+            return O.qg_search_batch(qg, h_rows, h_q[lo:hi], seeds[lo:hi], args.k, eps, args.expansion,
+                                     lut[lo:hi], sc[lo:hi], to[lo:hi], threads=threads, L=L)
+        return O.search_batch(metric, h_rows, h_off, h_edges, h_q[lo:hi], seeds[lo:hi], args.k, np.float32(eps),
+                              edge_size=0, threads=threads, L=L)
+
+    # size the sample to the time budget from a short probe
+    nq = h_q.shape[0]
+    probe = min(nq, 2 * threads)
+    t0 = time.perf_counter()
+    outs = [run(0, probe)]
+    dt = time.perf_counter() - t0
+    done = probe
+    target = int(probe * max(0.0, args.cpu_seconds - dt) / max(dt, 1e-6))
+    t1 = time.perf_counter()
+    if target > 0 and done < nq:
+        hi = min(nq, done + max(threads, target // threads * threads))
+        outs.append(run(done, hi))
+        done = hi
+    el = dt + (time.perf_counter() - t1)
+    ci = np.concatenate([o[0] for o in outs])
+    cd = np.concatenate([o[1] for o in outs])
+    cn = np.concatenate([o[2] for o in outs])
+    cc = np.concatenate([o[3] for o in outs])
+    gi, gd, gn = gpu_out
+    same = bool(np.array_equal(cn, gn[:done]))
+    for i in (range(done) if same else ()):
+        n = int(cn[i])
+        if not (np.array_equal(ci[i, :n], gi[i, :n]) and
+                np.array_equal(cd[i, :n].view(np.uint32), gd[i, :n].view(np.uint32))):
+            same = False
+            log("parity sample: query %d differs: cpu %s / gpu %s" % (i, ci[i, :n].tolist(), gi[i, :n].tolist()))
+            break
+    if qg is not None:
+        # ADC distances, accepted, expansions, exact distances: the same work
+        cnt_same = bool(np.array_equal(cc[:, :4], gpu_cnt[:done, :4].astype(np.uint64)))
+    else:
+        # distinct distance computations (the full-visited-set run's counters)
+        cnt_same = bool(np.array_equal(cc[:, 0], gpu_cnt[:done, 0].astype(np.uint64)))
+    parity = {"queries": done, "identical": same, "work_counters_identical": cnt_same,
+              "checked": "ids, float32 distance bits, result counts" + (
+                  ", ADC/accepted/expansion/exact counts" if qg is not None else ", distinct distance counts")}
+    if not (same and cnt_same):
+        raise SystemExit("bench: the device results differ from the oracle on the parity sample: %s" % parity)
+    log("parity sample: %d queries identical to the oracle (ids, distance bits, work counters)" % done)
     what = ("NGTQG::Index::searchQuantizedGraph restatement (LUT as input)" if qg is not None
             else "searchReadOnlyGraph restatement")
-    return {"value": done / el, "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": "%d of the %d queries (same graph, seeds, epsilon), oracle/ngt_oracle.c %s, 1 thread, %.1f s"
-                      % (done, h_q.shape[0], what, el)}
-
-
-def oracle_qg_search(O, qg, rows, q, seeds, k, eps, expansion, lut, sc, to):
-    L = O.lib()
-    O._qg_sigs(L)
-    p = O._p
-    ids = np.zeros(max(k, int(k * expansion) + 1), np.uint32)
-    ds = np.zeros_like(ids, dtype=np.float32)
-    cnt = np.zeros(4, np.uint64)
-    q = np.ascontiguousarray(q, np.float32)
-    s = np.ascontiguousarray(seeds, np.uint32)
-    L.ngto_qg_search(p(rows, ctypes.c_float), rows.shape[1], rows.shape[0], p(qg["qoff"], ctypes.c_uint64),
-                     p(qg["qids"], ctypes.c_uint32), p(qg["code_off"], ctypes.c_uint64),
-                     p(qg["codes"], ctypes.c_uint8), qg["M"], p(np.ascontiguousarray(lut), ctypes.c_uint8),
-                     float(sc), float(to), p(q, ctypes.c_float), p(s, ctypes.c_uint32), len(s), k, eps, expansion,
-                     3.402823466e38, p(ids, ctypes.c_uint32), p(ds, ctypes.c_float), p(cnt, ctypes.c_uint64))
+    base = {"value": done / el, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": "first %d of the %d queries (same graph, seeds, epsilon), oracle/ngt_oracle.c %s built -O3 "
+                      "-march=x86-64-%s (16-lane FMA order kept), one query per thread on %d threads, %.1f s; "
+                      "host: %s, %d CPUs" % (done, nq, what, isa, threads, el, model, ncpu)}
+    return base, parity
 
 
 if __name__ == "__main__":

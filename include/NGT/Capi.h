@@ -6,13 +6,18 @@
  * (false / NULL / 0 plus "Capi : <func>() : Error: <what>" in the NGTError
  * string, lib/NGT/Capi.cpp:25-38) are those of the reference, so a program or
  * binding written against libngt links against libngt_amd.so unchanged for
- * the paths this build implements (open / search / linear search / object
- * access / save / properties / results / errors).  Index construction and
- * graph-maintenance entry points are declared for link compatibility and
- * report an error until their rows of SURVEY.md section 8(f) land.
+ * the paths this build implements (open / create / append / ANNG construction
+ * / search / linear search / object access / save / properties / results /
+ * errors).  Graph-maintenance entry points (remove, optimizer, refine) are
+ * declared for link compatibility and report an error (out of scope).
+ *
+ * Threading: any number of threads may search one handle concurrently, as with
+ * the reference (Capi.cpp:377-406).  Concurrent single-query calls with equal
+ * parameters are coalesced into one device launch (ngt_amd/csrc/coalesce.h;
+ * NGT_AMD_COALESCE=0 turns it off).
  *
  * Extensions (not in the reference): ngt_batch_search_index*,
- * ngt_get_last_search_counters.
+ * ngt_get_last_search_counters, ngt_get_coalesce_stats.
  */
 #ifndef NGT_AMD_CAPI_H
 #define NGT_AMD_CAPI_H
@@ -134,6 +139,11 @@ NGTAnngEdgeOptimizationParameter ngt_get_anng_edge_optimization_parameter(void);
 bool ngt_optimize_number_of_edges(const char *indexPath, NGTAnngEdgeOptimizationParameter parameter,
                                   NGTError error);
 
+/* ---- extensions: distance types the reference sets only through the C++
+ * NGT::Property (ngtpy.cpp:79-94 "Normalized L2"; SparseJaccard, Index.cpp:488-490) */
+bool ngt_set_property_distance_type_normalized_l2(NGTProperty, NGTError);
+bool ngt_set_property_distance_type_sparse_jaccard(NGTProperty, NGTError);
+
 /* ---- extensions: batched device search ---------------------------------- */
 /* queries: [nq][dim] floats.  ids/dists: [nq][size], n: [nq] (results per query). */
 bool ngt_batch_search_index(NGTIndex, const float *queries, uint32_t nq, int32_t dim, size_t size,
@@ -146,9 +156,17 @@ bool ngt_batch_search_index_using_only_graph(NGTIndex, const float *queries, uin
                                              uint32_t *n, NGTError);
 bool ngt_batch_linear_search_index(NGTIndex, const float *queries, uint32_t nq, int32_t dim,
                                    size_t size, uint32_t *ids, float *dists, uint32_t *n, NGTError);
-/* counters of the last search on this handle: [0] distance computations,
- * [1] evaluated neighbours, [2] expansions (summed over its queries) */
+/* as above with SearchContainer::radius (< 0: unbounded), the form ngtpy's
+ * linear_search uses (ngtpy.cpp:236-242) */
+bool ngt_batch_linear_search_index_with_radius(NGTIndex, const float *queries, uint32_t nq,
+                                               int32_t dim, size_t size, float radius, uint32_t *ids,
+                                               float *dists, uint32_t *n, NGTError);
+/* counters of this thread's last search on this handle: [0] distance
+ * computations, [1] evaluated neighbours, [2] expansions (summed over its queries) */
 bool ngt_get_last_search_counters(NGTIndex, uint64_t *counters3, NGTError);
+/* single-query calls served so far: device launches issued and queries served
+ * by them (served / batches = mean coalesced batch size) */
+bool ngt_get_coalesce_stats(NGTIndex, uint64_t *batches, uint64_t *served, NGTError);
 
 #ifdef __cplusplus
 }

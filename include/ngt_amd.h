@@ -163,6 +163,9 @@ int ngt_amd_prepare_queries_device(ngt_amd_index *index, const float *d_in, uint
 
 /* Timing of the last search call's kernels (HIP events on the search stream), ms. */
 float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
+/* Workgroups (resident one-wave query slots) of the last search launch: per-CU
+ * occupancy x CUs for a full batch, bounded by the visited-scratch HBM budget. */
+uint32_t ngt_amd_last_search_slots(const ngt_amd_index *index);
 
 /* ---- ANNG construction --------------------------------------------------- *
  *   ngt_amd_build_begin / _insert <- GraphAndTreeIndex::createIndex(threadPoolSize)

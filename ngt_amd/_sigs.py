@@ -68,6 +68,7 @@ def declare(L):
         "ngt_amd_distances": (c_int, [vp, vp, c_uint32, vp, vp, c_uint64, vp]),
         "ngt_amd_prepare_queries_device": (c_int, [vp, vp, c_uint32, vp, vp]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
+        "ngt_amd_last_search_slots": (c_uint32, [vp]),
         "ngt_amd_build_begin": (c_int, [vp, POINTER(BuildParams)]),
         "ngt_amd_build_insert": (c_int, [vp, c_uint64, c_uint64]),
         "ngt_amd_build_graph_size": (c_int, [vp, u64p, u64p]),
@@ -116,6 +117,8 @@ def declare(L):
         "ngt_set_property_distance_type_cosine": (c_bool, [vp, vp]),
         "ngt_set_property_distance_type_normalized_angle": (c_bool, [vp, vp]),
         "ngt_set_property_distance_type_normalized_cosine": (c_bool, [vp, vp]),
+        "ngt_set_property_distance_type_normalized_l2": (c_bool, [vp, vp]),
+        "ngt_set_property_distance_type_sparse_jaccard": (c_bool, [vp, vp]),
         "ngt_create_empty_results": (vp, [vp]),
         "ngt_search_index": (c_bool, [vp, POINTER(c_double), c_int32, c_size_t, c_float, c_float, vp, vp]),
         "ngt_search_index_as_float": (c_bool, [vp, f32p, c_int32, c_size_t, c_float, c_float, vp, vp]),
@@ -155,7 +158,10 @@ def declare(L):
                                                              c_float, c_int64, u32p, f32p, u32p, vp]),
         "ngt_batch_linear_search_index": (c_bool, [vp, f32p, c_uint32, c_int32, c_size_t, u32p, f32p, u32p,
                                                    vp]),
+        "ngt_batch_linear_search_index_with_radius": (c_bool, [vp, f32p, c_uint32, c_int32, c_size_t, c_float,
+                                                               u32p, f32p, u32p, vp]),
         "ngt_get_last_search_counters": (c_bool, [vp, u64p, vp]),
+        "ngt_get_coalesce_stats": (c_bool, [vp, u64p, u64p, vp]),
         # ---- include/NGT/NGTQ/Capi.h
         "ngtqg_open_index": (vp, [c_char_p, vp]),
         "ngtqg_close_index": (None, [vp]),

@@ -38,6 +38,8 @@ class Index(object):
         self.otype = L.ngt_get_property_object_type(self.prop, self.err)
         self.is_float = bool(L.ngt_is_property_object_type_float(self.otype))
         self.distance_type = L.ngt_get_property_distance_type(self.prop, self.err)
+        # SparseJaccard objects keep one more slot (Index.cpp:488-490)
+        self.object_dim = self.dim + (1 if self.distance_type == 8 else 0)
         self.ospace = L.ngt_get_object_space(self.index, self.err)
 
     def _check(self, ok, err):
@@ -63,7 +65,9 @@ class Index(object):
                    "Jaccard": L.ngt_set_property_distance_type_jaccard,
                    "Cosine": L.ngt_set_property_distance_type_cosine,
                    "Normalized Angle": L.ngt_set_property_distance_type_normalized_angle,
-                   "Normalized Cosine": L.ngt_set_property_distance_type_normalized_cosine}
+                   "Normalized Cosine": L.ngt_set_property_distance_type_normalized_cosine,
+                   "Normalized L2": L.ngt_set_property_distance_type_normalized_l2,
+                   "Sparse Jaccard": L.ngt_set_property_distance_type_sparse_jaccard}
         ok = ok and setters[distance_type](prop, err)
         index = L.ngt_create_graph_and_tree(path.encode(), prop, err) if ok else None
         msg = _err_string(L, err)
@@ -141,32 +145,49 @@ class Index(object):
             L.ngt_destroy_results(results)
             L.ngt_destroy_error_object(err)
 
+    def _batch(self, queries):
+        """[nq][object dimension] float32 queries; a wrong length is an error,
+        as allocateObject's dimension check makes it (ObjectRepository.h:228-233)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2:
+            raise NativeError("queries must be a 2-d array")
+        if q.shape[1] != self.object_dim:
+            if self.distance_type == 8 and q.shape[1] < self.object_dim:
+                q = np.ascontiguousarray(np.pad(q, ((0, 0), (0, self.object_dim - q.shape[1]))))
+            else:
+                raise NativeError("The dimensionality is invalid. The indexed objects=%d The specified object=%d"
+                                  % (self.dim, q.shape[1]))
+        return q
+
     def batch_search(self, queries, k=20, epsilon=0.1, radius=-1.0, edge_size=-1, graph_only=False):
         """Batched search on the device: returns (ids[nq,k], dists[nq,k], n[nq])."""
         L = self._L
-        q = np.ascontiguousarray(queries, dtype=np.float32)
+        q = self._batch(queries)
         nq = q.shape[0]
         ids = np.zeros((nq, k), np.uint32)
         ds = np.zeros((nq, k), np.float32)
         n = np.zeros(nq, np.uint32)
         fn = L.ngt_batch_search_index_using_only_graph if graph_only else L.ngt_batch_search_index
-        ok = fn(self.index, q.ctypes.data_as(POINTER(c_float)), nq, self.dim, k, epsilon, radius, edge_size,
+        ok = fn(self.index, q.ctypes.data_as(POINTER(c_float)), nq, q.shape[1], k, epsilon, radius, edge_size,
                 ids.ctypes.data_as(POINTER(c_uint32)), ds.ctypes.data_as(POINTER(c_float)),
                 n.ctypes.data_as(POINTER(c_uint32)), self.err)
         self._check(ok, self.err)
         return ids, ds, n
 
-    def batch_linear_search(self, queries, k=20):
+    def batch_linear_search(self, queries, k=20, radius=-1.0):
+        """Exact k-NN of a batch (linearSearch with SearchContainer::radius;
+        radius < 0 is unbounded)."""
         L = self._L
-        q = np.ascontiguousarray(queries, dtype=np.float32)
+        q = self._batch(queries)
         nq = q.shape[0]
         ids = np.zeros((nq, k), np.uint32)
         ds = np.zeros((nq, k), np.float32)
         n = np.zeros(nq, np.uint32)
-        ok = L.ngt_batch_linear_search_index(self.index, q.ctypes.data_as(POINTER(c_float)), nq, self.dim, k,
-                                             ids.ctypes.data_as(POINTER(c_uint32)),
-                                             ds.ctypes.data_as(POINTER(c_float)),
-                                             n.ctypes.data_as(POINTER(c_uint32)), self.err)
+        ok = L.ngt_batch_linear_search_index_with_radius(self.index, q.ctypes.data_as(POINTER(c_float)), nq,
+                                                         q.shape[1], k, radius,
+                                                         ids.ctypes.data_as(POINTER(c_uint32)),
+                                                         ds.ctypes.data_as(POINTER(c_float)),
+                                                         n.ctypes.data_as(POINTER(c_uint32)), self.err)
         self._check(ok, self.err)
         return ids, ds, n
 

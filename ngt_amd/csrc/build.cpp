@@ -393,6 +393,9 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     HIP_OK(hipMemcpyAsync(hc, b.counts.p, sizeof hc, hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
+    int serr = 0;  // the insertion searches' flag (their launch context on s)
+    if (take_device_error(ix, s, &serr)) return -1;
+    herr |= serr;
     if (herr) {
       (void)hipMemset(ix->error.p, 0, sizeof(int));
       return fail("ngt_amd_build_insert: device error flag %d (1 unchecked-set spill full; DVP tree: 2 already "

@@ -12,12 +12,15 @@
 #include <sys/stat.h>
 
 #include <iostream>
+#include <memory>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "../../include/NGT/Capi.h"
 #include "../../include/ngt_amd.h"
+#include "coalesce.h"
 #include "index_io.h"
 
 using ngt_amd::HostIndex;
@@ -29,11 +32,16 @@ struct CapiIndex {
   HostIndex host;
   ngt_amd_index* dev = nullptr;
   bool device_stale = true;
-  uint64_t last_counters[3] = {0, 0, 0};
+  std::mutex mu;                           // device (re)build and host mutations
+  std::unique_ptr<ngt_amd::Coalescer> co;  // concurrent single-query callers
   ~CapiIndex() {
     if (dev) ngt_amd_index_destroy(dev);
   }
 };
+
+// The last search's counters are per calling thread: concurrent callers of
+// one handle each read their own (ngt_get_last_search_counters).
+thread_local uint64_t t_last_counters[3] = {0, 0, 0};
 
 typedef std::vector<NGTObjectDistance> Results;
 
@@ -63,6 +71,7 @@ std::string amd_err() { return std::string(ngt_amd_last_error()); }
 
 // Build / refresh the device index from the host mirror.
 std::string sync_device(CapiIndex* ix) {
+  std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->device_stale && ix->dev) return "";
   HostIndex& h = ix->host;
   if (h.nrows < 2) return "the index is empty";
@@ -71,7 +80,7 @@ std::string sync_device(CapiIndex* ix) {
     const char* env = getenv("NGT_AMD_DEVICE");
     if (env) dev = atoi(env);
     if (ngt_amd_index_create(&ix->dev, dev, h.prop.distance_type, h.prop.object_type,
-                             (uint32_t)h.prop.dimension))
+                             (uint32_t)h.prop.object_dimension()))
       return amd_err();
   }
   if (ngt_amd_index_set_objects(ix->dev, h.rows.data(), h.nrows, h.valid.data())) return amd_err();
@@ -97,7 +106,8 @@ bool use_tree(CapiIndex* ix) { return ix->host.prop.index_type == 0 && ix->host.
 // One batched search: the single-query API is a batch of one.
 std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t size, float epsilon,
                        float radius, int64_t edge_size, int seed_mode, std::vector<uint32_t>& ids,
-                       std::vector<float>& dists, std::vector<uint32_t>& n) {
+                       std::vector<float>& dists, std::vector<uint32_t>& n,
+                       std::vector<uint64_t>* per_query = nullptr) {
   std::string e = sync_device(ix);
   if (!e.empty()) return e;
   if (size == 0) {
@@ -119,14 +129,16 @@ std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t 
   if (ngt_amd_search(ix->dev, &p, queries, nq, nullptr, nullptr, ids.data(), dists.data(), n.data(),
                      cnt.data()))
     return amd_err();
-  ix->last_counters[0] = ix->last_counters[1] = ix->last_counters[2] = 0;
+  t_last_counters[0] = t_last_counters[1] = t_last_counters[2] = 0;
   for (uint32_t q = 0; q < nq; q++)
-    for (int c = 0; c < 3; c++) ix->last_counters[c] += cnt[(size_t)q * NGT_AMD_COUNTERS_PER_QUERY + c];
+    for (int c = 0; c < 3; c++) t_last_counters[c] += cnt[(size_t)q * NGT_AMD_COUNTERS_PER_QUERY + c];
+  if (per_query) *per_query = std::move(cnt);
   return "";
 }
 
 std::string run_linear(CapiIndex* ix, const float* queries, uint32_t nq, size_t size,
-                       std::vector<uint32_t>& ids, std::vector<float>& dists, std::vector<uint32_t>& n) {
+                       std::vector<uint32_t>& ids, std::vector<float>& dists, std::vector<uint32_t>& n,
+                       double radius = (double)FLT_MAX) {
   std::string e = sync_device(ix);
   if (!e.empty()) return e;
   if (size == 0) {
@@ -136,8 +148,9 @@ std::string run_linear(CapiIndex* ix, const float* queries, uint32_t nq, size_t 
   ids.resize((size_t)nq * size);
   dists.resize((size_t)nq * size);
   n.resize(nq);
-  // sc.radius stays FLT_MAX in ngt_linear_search_index_ (Capi.cpp:441-456)
-  if (ngt_amd_linear_search(ix->dev, queries, nq, (uint32_t)size, (double)FLT_MAX, ids.data(),
+  // sc.radius stays FLT_MAX in ngt_linear_search_index_ (Capi.cpp:441-456);
+  // ngtpy passes its default radius (ngtpy.cpp:238)
+  if (ngt_amd_linear_search(ix->dev, queries, nq, (uint32_t)size, radius, ids.data(),
                             dists.data(), n.data()))
     return amd_err();
   return "";
@@ -165,25 +178,60 @@ std::string create_empty(CapiIndex* ix, const HostProperty& prop) {
   return "";
 }
 
+// ObjectSpace::normalize (ObjectSpace.h:251-266) of one stored object, with
+// the arithmetic of the device query preparation (prep_kernels.hip: 16 FMA
+// lanes over the unpadded dimension, 8/4/2/1 fold, FMA tail, sqrtf, divide),
+// so an inserted object and the same vector given as a query normalize to
+// the same bits.
+template <typename T>
+std::string normalize_row(T* data, uint32_t dim) {
+  float acc[16] = {0};
+  const uint32_t main = dim & ~15u;
+  for (uint32_t i = 0; i < main; i++) acc[i & 15] = fmaf((float)data[i], (float)data[i], acc[i & 15]);
+  for (int w = 8; w >= 1; w >>= 1)
+    for (int l = 0; l < w; l++) acc[l] = acc[l + w] + acc[l];
+  float sum = acc[0];
+  for (uint32_t i = main; i < dim; i++) sum = fmaf((float)data[i], (float)data[i], sum);
+  if (sum == 0.0f)
+    return "ObjectSpace::normalize: Error! the object is an invalid zero vector for the cosine similarity or "
+           "normalized distances.";
+  const float scale = sqrtf(sum);
+  for (uint32_t i = 0; i < dim; i++) data[i] = static_cast<T>((float)data[i] / scale);
+  return "";
+}
+
 // Append one object to the host mirror, converting like
-// ObjectRepository::allocateObject (ObjectRepository.h:222-253).  The
-// normalization of stored objects for normalized metrics is part of index
-// construction and is rejected here.
+// ObjectRepository::allocateObject (ObjectRepository.h:222-253) and, for the
+// normalized metrics, normalizing like allocateNormalizedObject
+// (ObjectSpaceRepository.h:560-566).
 template <typename T>
 std::string append_object(CapiIndex* ix, const T* obj, uint32_t dim, uint32_t& id) {
+  std::lock_guard<std::mutex> lk(ix->mu);
   HostIndex& h = ix->host;
-  if ((int32_t)dim != h.prop.dimension) return "the specified dimension is invalid";
-  int m = h.prop.distance_type;
-  if (m == 5 || m == 6 || m == 9) return "inserting into normalized-distance indexes is not implemented";
-  id = (uint32_t)h.nrows;
-  h.rows.resize((h.nrows + 1) * h.row_bytes, 0);
-  uint8_t* row = h.rows.data() + h.nrows * h.row_bytes;
+  const bool sparse = h.prop.distance_type == 8;
+  // a sparse object (0-terminated id list, Index::makeSparseObject) may be
+  // shorter than the object dimension (ObjectRepository.h:222-233)
+  if (sparse ? (int32_t)dim > h.prop.object_dimension() : (int32_t)dim != h.prop.dimension)
+    return "the specified dimension is invalid";
+  const int m = h.prop.distance_type;
+  const bool normalized = m == 5 || m == 6 || m == 9;
+  std::vector<uint8_t> row(h.row_bytes, 0);
   if (h.prop.object_type == 2) {
-    float* f = reinterpret_cast<float*>(row);
+    float* f = reinterpret_cast<float*>(row.data());
     for (uint32_t i = 0; i < dim; i++) f[i] = static_cast<float>(obj[i]);
+    if (normalized) {
+      std::string e = normalize_row(f, dim);
+      if (!e.empty()) return e;
+    }
   } else {
     for (uint32_t i = 0; i < dim; i++) row[i] = static_cast<uint8_t>(obj[i]);
+    if (normalized) {
+      std::string e = normalize_row(row.data(), dim);
+      if (!e.empty()) return e;
+    }
   }
+  id = (uint32_t)h.nrows;
+  h.rows.insert(h.rows.end(), row.begin(), row.end());
   h.valid.push_back(1);
   h.nrows++;
   h.edge_off.push_back(h.edge_off.back());
@@ -418,6 +466,8 @@ SET_DIST(ngt_set_property_distance_type_jaccard, 7)
 SET_DIST(ngt_set_property_distance_type_cosine, 4)
 SET_DIST(ngt_set_property_distance_type_normalized_angle, 5)
 SET_DIST(ngt_set_property_distance_type_normalized_cosine, 6)
+SET_DIST(ngt_set_property_distance_type_normalized_l2, 9)
+SET_DIST(ngt_set_property_distance_type_sparse_jaccard, 8)
 #undef SET_DIST
 
 int16_t ngt_get_property_edge_size_for_creation(NGTProperty prop, NGTError error) {
@@ -442,19 +492,88 @@ NGTObjectDistances ngt_create_empty_results(NGTError error) {
   }
 }
 
+static ngt_amd::Coalescer* coalescer_of(CapiIndex* ix) {
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->co) ix->co.reset(new ngt_amd::Coalescer((uint32_t)ix->host.prop.object_dimension()));
+  return ix->co.get();
+}
+
+// The query as the device takes it: object_dimension floats (a sparse query
+// shorter than that is zero-padded; other metrics need the exact dimension).
+static bool query_of(CapiIndex* ix, const float* q, int32_t qdim, std::vector<float>& out) {
+  const HostProperty& p = ix->host.prop;
+  if (p.distance_type == 8 ? (qdim > p.object_dimension()) : (qdim != p.dimension)) return false;
+  out.assign(q, q + qdim);
+  out.resize(p.object_dimension(), 0.0f);
+  return true;
+}
+
+enum { kGraphSearch = 0, kLinearSearch = 1 };
+
+// One single-query call: joins the batch of concurrent callers with the same
+// parameters (coalesce.h), or runs alone when coalescing is off.
+static std::string single_query(CapiIndex* ix, int kind, const float* q, size_t size, float epsilon, float radius,
+                                int64_t edge_size, int seed_mode, std::vector<uint32_t>& ids,
+                                std::vector<float>& dists, uint32_t& n) {
+  if (!ngt_amd::coalesce_enabled()) {
+    std::vector<uint32_t> vn;
+    std::string e = kind == kGraphSearch
+                        ? run_search(ix, q, 1, size, epsilon, radius, edge_size, seed_mode, ids, dists, vn)
+                        : run_linear(ix, q, 1, size, ids, dists, vn);
+    n = vn.empty() ? 0 : vn[0];
+    return e;
+  }
+  ngt_amd::CoalesceReq r;
+  r.key.kind = kind;
+  r.key.size = (uint32_t)size;
+  r.key.epsilon = epsilon;
+  r.key.radius = radius;
+  r.key.edge_size = edge_size;
+  r.key.seed_mode = seed_mode;
+  r.query = q;
+  coalescer_of(ix)->submit(&r, [ix](const ngt_amd::CoalesceKey& k, const float* qs, uint32_t nq,
+                                    std::vector<ngt_amd::CoalesceReq*>& batch) {
+    std::vector<uint32_t> vi, vn;
+    std::vector<float> vd;
+    std::vector<uint64_t> cnt;
+    std::string e = k.kind == kGraphSearch
+                        ? run_search(ix, qs, nq, k.size, k.epsilon, k.radius, k.edge_size, k.seed_mode, vi, vd, vn,
+                                     &cnt)
+                        : run_linear(ix, qs, nq, k.size, vi, vd, vn);
+    for (uint32_t i = 0; i < nq; i++) {
+      ngt_amd::CoalesceReq* b = batch[i];
+      b->err = e;
+      if (!e.empty()) continue;
+      b->n = vn[i];
+      b->ids.assign(vi.begin() + (size_t)i * k.size, vi.begin() + (size_t)i * k.size + vn[i]);
+      b->dists.assign(vd.begin() + (size_t)i * k.size, vd.begin() + (size_t)i * k.size + vn[i]);
+      if (!cnt.empty())
+        for (int c = 0; c < 3; c++) b->counters[c] = cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + c];
+    }
+  });
+  if (r.err.empty()) {
+    ids.swap(r.ids);
+    dists.swap(r.dists);
+    n = r.n;
+    if (kind == kGraphSearch) memcpy(t_last_counters, r.counters, sizeof r.counters);
+  }
+  return r.err;
+}
+
 static bool search_one(const char* func, NGTIndex index, const float* q, size_t size, float epsilon,
                        float radius, int64_t edge_size, NGTObjectDistances results, NGTError error) {
   CapiIndex* ix = static_cast<CapiIndex*>(index);
-  std::vector<uint32_t> ids, n;
+  std::vector<uint32_t> ids;
   std::vector<float> dists;
+  uint32_t n = 0;
   if (radius < 0.0f) radius = FLT_MAX;  // Capi.cpp:357-359
-  std::string e = run_search(ix, q, 1, size, epsilon, radius, edge_size,
-                             use_tree(ix) ? NGT_AMD_SEED_TREE : NGT_AMD_SEED_RANDOM, ids, dists, n);
+  std::string e = single_query(ix, kGraphSearch, q, size, epsilon, radius, edge_size,
+                               use_tree(ix) ? NGT_AMD_SEED_TREE : NGT_AMD_SEED_RANDOM, ids, dists, n);
   if (!e.empty()) {
     set_error(error, func, e);
     return false;
   }
-  fill_results(results, ids, dists, n.empty() ? 0 : n[0]);
+  fill_results(results, ids, dists, n);
   return true;
 }
 
@@ -466,8 +585,8 @@ bool ngt_search_index(NGTIndex index, double* query, int32_t query_dim, size_t s
     param_error(error, __FUNCTION__, ss.str());
     return false;
   }
-  std::vector<float> q(query, query + query_dim);
-  if (query_dim != static_cast<CapiIndex*>(index)->host.prop.dimension) {
+  std::vector<float> qf(query, query + query_dim), q;
+  if (!query_of(static_cast<CapiIndex*>(index), qf.data(), query_dim, q)) {
     set_error(error, __FUNCTION__, "the specified dimension is invalid");
     return false;
   }
@@ -482,11 +601,12 @@ bool ngt_search_index_as_float(NGTIndex index, float* query, int32_t query_dim, 
     param_error(error, __FUNCTION__, ss.str());
     return false;
   }
-  if (query_dim != static_cast<CapiIndex*>(index)->host.prop.dimension) {
+  std::vector<float> q;
+  if (!query_of(static_cast<CapiIndex*>(index), query, query_dim, q)) {
     set_error(error, __FUNCTION__, "the specified dimension is invalid");
     return false;
   }
-  return search_one(__FUNCTION__, index, query, size, epsilon, radius, -1, results, error);
+  return search_one(__FUNCTION__, index, q.data(), size, epsilon, radius, -1, results, error);
 }
 
 bool ngt_search_index_with_query(NGTIndex index, NGTQuery query, NGTObjectDistances results, NGTError error) {
@@ -496,21 +616,25 @@ bool ngt_search_index_with_query(NGTIndex index, NGTQuery query, NGTObjectDistan
     param_error(error, __FUNCTION__, ss.str());
     return false;
   }
-  return search_one(__FUNCTION__, index, query.query, query.size, query.epsilon, query.radius,
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  std::vector<float> q;
+  query_of(ix, query.query, ix->host.prop.dimension, q);  // NGTQuery carries no dimension: the index's
+  return search_one(__FUNCTION__, index, q.data(), query.size, query.epsilon, query.radius,
                     (int64_t)(int)query.edge_size, results, error);
 }
 
 static bool linear_one(const char* func, NGTIndex index, const float* q, size_t size,
                        NGTObjectDistances results, NGTError error) {
   CapiIndex* ix = static_cast<CapiIndex*>(index);
-  std::vector<uint32_t> ids, n;
+  std::vector<uint32_t> ids;
   std::vector<float> dists;
-  std::string e = run_linear(ix, q, 1, size, ids, dists, n);
+  uint32_t n = 0;
+  std::string e = single_query(ix, kLinearSearch, q, size, 0.f, FLT_MAX, 0, 0, ids, dists, n);
   if (!e.empty()) {
     set_error(error, func, e);
     return false;
   }
-  fill_results(results, ids, dists, n.empty() ? 0 : n[0]);
+  fill_results(results, ids, dists, n);
   return true;
 }
 
@@ -522,7 +646,11 @@ bool ngt_linear_search_index(NGTIndex index, double* query, int32_t query_dim, s
     param_error(error, __FUNCTION__, ss.str());
     return false;
   }
-  std::vector<float> q(query, query + query_dim);
+  std::vector<float> qf(query, query + query_dim), q;
+  if (!query_of(static_cast<CapiIndex*>(index), qf.data(), query_dim, q)) {
+    set_error(error, __FUNCTION__, "the specified dimension is invalid");
+    return false;
+  }
   return linear_one(__FUNCTION__, index, q.data(), size, results, error);
 }
 
@@ -534,7 +662,12 @@ bool ngt_linear_search_index_as_float(NGTIndex index, float* query, int32_t quer
     param_error(error, __FUNCTION__, ss.str());
     return false;
   }
-  return linear_one(__FUNCTION__, index, query, size, results, error);
+  std::vector<float> q;
+  if (!query_of(static_cast<CapiIndex*>(index), query, query_dim, q)) {
+    set_error(error, __FUNCTION__, "the specified dimension is invalid");
+    return false;
+  }
+  return linear_one(__FUNCTION__, index, q.data(), size, results, error);
 }
 
 bool ngt_linear_search_index_with_query(NGTIndex index, NGTQuery query, NGTObjectDistances results,
@@ -545,7 +678,10 @@ bool ngt_linear_search_index_with_query(NGTIndex index, NGTQuery query, NGTObjec
     param_error(error, __FUNCTION__, ss.str());
     return false;
   }
-  return linear_one(__FUNCTION__, index, query.query, query.size, results, error);
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  std::vector<float> q;
+  query_of(ix, query.query, ix->host.prop.dimension, q);
+  return linear_one(__FUNCTION__, index, q.data(), query.size, results, error);
 }
 
 int32_t ngt_get_size(NGTObjectDistances results, NGTError error) {
@@ -612,7 +748,7 @@ bool ngt_batch_append_index(NGTIndex index, float* obj, uint32_t data_count, NGT
     return false;
   }
   CapiIndex* ix = static_cast<CapiIndex*>(index);
-  uint32_t dim = (uint32_t)ix->host.prop.dimension, id;
+  uint32_t dim = (uint32_t)ix->host.prop.object_dimension(), id;
   for (uint32_t i = 0; i < data_count; i++) {
     std::string e = append_object(ix, obj + (size_t)i * dim, dim, id);
     if (!e.empty()) {
@@ -810,7 +946,7 @@ static bool batch_search(const char* func, NGTIndex index, const float* queries,
     return false;
   }
   CapiIndex* ix = static_cast<CapiIndex*>(index);
-  if (dim != ix->host.prop.dimension) {
+  if (dim != ix->host.prop.object_dimension()) {  // batches are [nq][object dimension]
     set_error(error, func, "the specified dimension is invalid");
     return false;
   }
@@ -845,18 +981,24 @@ bool ngt_batch_search_index_using_only_graph(NGTIndex index, const float* querie
 
 bool ngt_batch_linear_search_index(NGTIndex index, const float* queries, uint32_t nq, int32_t dim, size_t size,
                                    uint32_t* ids, float* dists, uint32_t* n, NGTError error) {
+  return ngt_batch_linear_search_index_with_radius(index, queries, nq, dim, size, FLT_MAX, ids, dists, n, error);
+}
+
+bool ngt_batch_linear_search_index_with_radius(NGTIndex index, const float* queries, uint32_t nq, int32_t dim,
+                                               size_t size, float radius, uint32_t* ids, float* dists, uint32_t* n,
+                                               NGTError error) {
   if (index == NULL || queries == NULL || ids == NULL || dists == NULL || n == NULL) {
     param_error(error, __FUNCTION__, "null argument");
     return false;
   }
   CapiIndex* ix = static_cast<CapiIndex*>(index);
-  if (dim != ix->host.prop.dimension) {
+  if (dim != ix->host.prop.object_dimension()) {
     set_error(error, __FUNCTION__, "the specified dimension is invalid");
     return false;
   }
   std::vector<uint32_t> vi, vn;
   std::vector<float> vd;
-  std::string e = run_linear(ix, queries, nq, size, vi, vd, vn);
+  std::string e = run_linear(ix, queries, nq, size, vi, vd, vn, radius < 0.0f ? -1.0 : (double)radius);
   if (!e.empty()) {
     set_error(error, __FUNCTION__, e);
     return false;
@@ -872,7 +1014,16 @@ bool ngt_get_last_search_counters(NGTIndex index, uint64_t* counters3, NGTError 
     param_error(error, __FUNCTION__, "null argument");
     return false;
   }
-  memcpy(counters3, static_cast<CapiIndex*>(index)->last_counters, 3 * sizeof(uint64_t));
+  memcpy(counters3, t_last_counters, 3 * sizeof(uint64_t));
+  return true;
+}
+
+bool ngt_get_coalesce_stats(NGTIndex index, uint64_t* batches, uint64_t* served, NGTError error) {
+  if (index == NULL || batches == NULL || served == NULL) {
+    param_error(error, __FUNCTION__, "null argument");
+    return false;
+  }
+  coalescer_of(static_cast<CapiIndex*>(index))->stats(batches, served);
   return true;
 }
 

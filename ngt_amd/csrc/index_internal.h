@@ -6,6 +6,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -41,6 +43,12 @@ struct DevBuf {
     n = count;
     return hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
   }
+  hipError_t upload_async(const T* h, size_t count, hipStream_t s) {
+    hipError_t e = alloc(count);
+    if (e != hipSuccess) return e;
+    if (count) e = hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s);
+    return e;
+  }
   hipError_t upload(const T* h, size_t count) {
     hipError_t e = alloc(count);
     if (e != hipSuccess) return e;
@@ -74,13 +82,32 @@ struct SearchCtx {
   DevBuf<uint64_t> seed_off, spill;
   DevBuf<uint8_t> vis;           // [slots][vis_stride] visited epochs
   uint32_t slots = 0;
+  uint32_t launch_slots = 0;     // workgroups (resident waves) of the last launch
   uint64_t vis_stride = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the search kernel
   DevBuf<uint8_t> lut;           // NGTQG: [nq][Me*16]
   DevBuf<float> scale, toff;
+  DevBuf<uint64_t> partial;      // linear search: [nq][nslices][k] slice top-k
+  DevBuf<int> err;               // device error flag of the launches on this stream
   ~SearchCtx() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+  }
+};
+
+// Buffers of one synchronous host-API call (ngt_amd_search, _linear_search,
+// _qg_search, ...): its own HIP stream, so concurrent callers run concurrent
+// launches, and device/pinned buffers kept across calls, so a call costs no
+// hipMalloc once warm.  Taken from and returned to the index's pool.
+struct CallCtx {
+  hipStream_t stream = nullptr;
+  DevBuf<float> raw;             // host float queries as uploaded
+  DevBuf<uint8_t> prep;          // prepared (converted, padded, normalized) rows
+  DevBuf<uint32_t> ids, n, seeds;
+  DevBuf<float> dists;
+  DevBuf<uint64_t> cnt, seed_off;
+  ~CallCtx() {
+    if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -167,14 +194,17 @@ struct ngt_amd_index {
   int32_t dyn_base = 30, dyn_rate = 20;
   int32_t seed_size = 10, seed_type = 0;
   // scratch
+  std::mutex mu;                           // guards ctxs, calls, rand() seeds
   std::vector<ngt_amd::SearchCtx*> ctxs;   // per launch stream
-  ngt_amd::SearchCtx* last_ctx = nullptr;  // context of the latest search
+  std::atomic<ngt_amd::SearchCtx*> last_ctx{nullptr};  // context of the latest search
+  std::vector<ngt_amd::CallCtx*> calls;    // idle host-API call contexts
   DevBuf<int> error;
   uint32_t spill_cap = 1u << 16;
   hipStream_t stream = nullptr;
   ngt_amd::BuildState* build = nullptr;    // ANNG construction (build.cpp)
   ~ngt_amd_index() {
     for (auto* c : ctxs) delete c;
+    for (auto* c : calls) delete c;
     delete build;
   }
   int cu_count = 256;
@@ -188,7 +218,21 @@ constexpr uint32_t kTreeSeedStride = 128;  // max seeds per query from a tree le
 
 // the launch context of stream s (created on first use), or null on failure
 SearchCtx* ctx_for(ngt_amd_index* ix, hipStream_t s);
-int ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds_per_slot, hipStream_t s);
+// per-slot visited scratch for a launch of nq queries (slots = resident waves)
+int ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds_per_slot, uint32_t nq, hipStream_t s);
+// device error flag of stream s's launches: read (synchronising s), clear, return
+int take_device_error(ngt_amd_index* ix, hipStream_t s, int* flag);
+// host-API call contexts (own stream + persistent buffers), pooled per index
+CallCtx* acquire_call(ngt_amd_index* ix);
+void release_call(ngt_amd_index* ix, CallCtx* c);
+struct CallGuard {
+  ngt_amd_index* ix;
+  CallCtx* c;
+  explicit CallGuard(ngt_amd_index* i) : ix(i), c(acquire_call(i)) {}
+  ~CallGuard() {
+    if (c) release_call(ix, c);
+  }
+};
 int run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queries, uint64_t query_bytes, uint32_t nq,
                    uint32_t k, int all_leaf_nodes, hipStream_t s);
 float coef_of(float epsilon);

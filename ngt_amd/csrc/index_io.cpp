@@ -168,7 +168,7 @@ void HostProperty::to_kv() {
 }
 
 void HostIndex::init_layout() {
-  dp = (uint32_t)(((prop.dimension - 1) / 16 + 1) * 16);
+  dp = (uint32_t)(((prop.object_dimension() - 1) / 16 + 1) * 16);
   esize = prop.object_type == 1 ? 1 : 4;
   row_bytes = (uint64_t)dp * esize;
 }
@@ -200,7 +200,7 @@ std::string load_index(const std::string& dir, HostIndex& ix) {
   std::string e = read_prf(dir + "/prf", ix.prop);
   if (!e.empty()) return e;
   ix.init_layout();
-  const size_t obytes = (size_t)ix.prop.dimension * ix.esize;
+  const size_t obytes = (size_t)ix.prop.object_dimension() * ix.esize;
   // ---- obj
   {
     Reader r;
@@ -321,7 +321,7 @@ std::string load_index(const std::string& dir, HostIndex& ix) {
 std::string save_index(const std::string& dir, HostIndex& ix) {
   std::string e = write_prf(dir + "/prf", ix.prop);
   if (!e.empty()) return e;
-  const size_t obytes = (size_t)ix.prop.dimension * ix.esize;
+  const size_t obytes = (size_t)ix.prop.object_dimension() * ix.esize;
   {
     Writer w(dir + "/obj");
     if (!w.f) return "cannot write obj";

@@ -35,6 +35,9 @@ struct HostProperty {
   int32_t batch_size_for_creation = 200;
   int32_t prefetch_offset = 0, prefetch_size = 0;
   void set_defaults();            // NGT::Property defaults (Index.h:45-104, Graph.h:386-402)
+  // the object space's dimension: SparseJaccard keeps one more slot for the
+  // 0 terminator (GraphIndex::constructObjectSpace, Index.cpp:484-490)
+  int32_t object_dimension() const { return dimension + (distance_type == 8 ? 1 : 0); }
   void from_kv();
   void to_kv();
 };

@@ -233,46 +233,103 @@ extern "C" uint64_t ngt_amd_resolve_edge_size(const ngt_amd_index* ix, int64_t e
   return 0;  // invalid -> caller reports
 }
 
-// Per-slot scratch of the persistent search kernels (slot = resident wave):
-// visited-epoch bytes, their epochs and the unchecked-set spill.  Sized by the
-// LDS footprint of one slot, which bounds how many are resident per CU.
+// Launch context of stream s: per-slot scratch of the persistent search
+// kernels (slot = resident wave), seed lists, events, error flag.  Created on
+// first use; the list is shared by every thread searching this index.
 ngt_amd::SearchCtx* ngt_amd::ctx_for(ngt_amd_index* ix, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(ix->mu);
   for (auto* c : ix->ctxs)
-    if (c->stream == s) return ix->last_ctx = c;
+    if (c->stream == s) {
+      ix->last_ctx = c;
+      return c;
+    }
   auto* c = new SearchCtx();
   c->stream = s;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      c->work.alloc(4) != hipSuccess) {
+      c->work.alloc(4) != hipSuccess || c->err.alloc(1) != hipSuccess ||
+      hipMemset(c->err.p, 0, sizeof(int)) != hipSuccess) {
     delete c;
     fail("search: cannot create the launch context of stream %p", (void*)s);
     return nullptr;
   }
   ix->ctxs.push_back(c);
-  return ix->last_ctx = c;
+  ix->last_ctx = c;
+  return c;
 }
 
-int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds, hipStream_t s) {
+int ngt_amd::take_device_error(ngt_amd_index* ix, hipStream_t s, int* flag) {
+  *flag = 0;
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
+  HIP_OK(hipMemcpyAsync(flag, c->err.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  if (*flag) HIP_OK(hipMemsetAsync(c->err.p, 0, sizeof(int), s));
+  return 0;
+}
+
+ngt_amd::CallCtx* ngt_amd::acquire_call(ngt_amd_index* ix) {
+  {
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (!ix->calls.empty()) {
+      CallCtx* c = ix->calls.back();
+      ix->calls.pop_back();
+      return c;
+    }
+  }
+  auto* c = new CallCtx();
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    fail("search: cannot create a call stream");
+    return nullptr;
+  }
+  return c;
+}
+
+void ngt_amd::release_call(ngt_amd_index* ix, CallCtx* c) {
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->calls.push_back(c);
+}
+
+// Visited epochs take slots x nrows bytes.  Slots = resident waves of the
+// launch (per_cu x CUs, fewer for small batches), bounded only by a share of
+// the free HBM (NGT_AMD_VIS_MEM_FRAC, default 0.45 of what is free): a
+// 12.5M-row shard keeps 16 waves per CU (51 GB of epochs on a 288 GB GPU).
+int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds, uint32_t nq, hipStream_t s) {
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
   static const uint32_t max_per_cu = [] {
     const char* v = getenv("NGT_AMD_WAVES_PER_CU");
     return v ? (uint32_t)std::max(1, std::min(32, atoi(v))) : 16u;
   }();
+  static const double mem_frac = [] {
+    const char* v = getenv("NGT_AMD_VIS_MEM_FRAC");
+    return v ? std::max(0.01, std::min(0.9, atof(v))) : 0.45;
+  }();
   if (per_cu > max_per_cu) per_cu = max_per_cu;
   if (per_cu < 1) per_cu = 1;
-  uint64_t stride = (ix->nrows + 15) & ~15ull;
-  // the per-slot visited epochs take slots * nrows bytes: keep them <= 16 GiB
-  uint64_t max_slots = (16ull << 30) / stride;
-  uint32_t slots = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * ix->cu_count, std::max<uint64_t>(max_slots, 64));
-  if (slots != c->slots || stride != c->vis_stride || !c->spill.p) {
-    HIP_OK(c->vis.alloc((size_t)slots * stride));
-    // zeroed on the launch stream so the first search is ordered after it
-    HIP_OK(hipMemsetAsync(c->vis.p, 0, (size_t)slots * stride, s));
-    HIP_OK(c->slot_epoch.alloc(slots));
-    HIP_OK(hipMemsetAsync(c->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t), s));
-    HIP_OK(c->spill.alloc((size_t)slots * ix->spill_cap));
-    c->slots = slots;
-    c->vis_stride = stride;
-  }
+  const uint64_t stride = (ix->nrows + 15) & ~15ull;
+  const uint32_t full = per_cu * (uint32_t)ix->cu_count;
+  // small launches (coalesced C-API calls) take slots in steps of 64
+  uint32_t want = std::min<uint32_t>(full, (nq + 63) & ~63u);
+  if (want < c->slots && stride == c->vis_stride && c->spill.p) return 0;  // never shrink
+  if (want == c->slots && stride == c->vis_stride && c->spill.p) return 0;
+  size_t freeb = 0, totalb = 0;
+  HIP_OK(hipMemGetInfo(&freeb, &totalb));
+  const double avail = (double)freeb + (double)c->vis.n + (double)c->spill.n * 8.0;
+  const uint64_t per_slot = stride + (uint64_t)ix->spill_cap * 8 + 4;
+  const uint64_t max_slots = (uint64_t)(avail * mem_frac) / per_slot;
+  if (max_slots < 1) return fail("search: no HBM left for the visited scratch (%llu rows)", (unsigned long long)ix->nrows);
+  const uint32_t slots = (uint32_t)std::min<uint64_t>(std::max(want, c->slots), max_slots);
+  if (slots == c->slots && stride == c->vis_stride && c->spill.p) return 0;
+  c->vis.release();
+  c->spill.release();
+  HIP_OK(c->vis.alloc((size_t)slots * stride));
+  // zeroed on the launch stream so the first search is ordered after it
+  HIP_OK(hipMemsetAsync(c->vis.p, 0, (size_t)slots * stride, s));
+  HIP_OK(c->slot_epoch.alloc(slots));
+  HIP_OK(hipMemsetAsync(c->slot_epoch.p, 0, (size_t)slots * sizeof(uint32_t), s));
+  HIP_OK(c->spill.alloc((size_t)slots * ix->spill_cap));
+  c->slots = slots;
+  c->vis_stride = stride;
   return 0;
 }
 
@@ -386,7 +443,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   a.out_dists = d_dists;
   a.out_n = d_n;
   a.counters = d_counters;
-  a.error = ix->error.p;
+  a.error = c->err.p;
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
     if (run_tree_seeds(ix, c, d_queries, query_bytes, nq, prm->k, prm->all_leaf_nodes, s)) return -1;
@@ -400,7 +457,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   }
   const size_t lds = search_lds_bytes(a, ix->otype);
   if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
-  if (ensure_vis_scratch(ix, c, lds, s)) return -1;
+  if (ensure_vis_scratch(ix, c, lds, nq, s)) return -1;
   a.vis = c->vis.p;
   a.vis_stride = c->vis_stride;
   a.slot_epoch = c->slot_epoch.p;
@@ -409,6 +466,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   a.work = c->work.p;
   HIP_OK(hipMemsetAsync(c->work.p, 0, sizeof(uint32_t), s));
   uint32_t slots = std::min<uint32_t>(c->slots, nq);
+  c->launch_slots = slots;
   HIP_OK(hipEventRecord(c->ev0, s));
   HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
   HIP_OK(hipEventRecord(c->ev1, s));
@@ -453,7 +511,11 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
   if (!c) return -1;
   if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
-    std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
+    std::vector<uint32_t> seeds;
+    {
+      std::lock_guard<std::mutex> lk(ix->mu);  // one query after another on the rand() stream
+      seeds = random_seed_lists(ix, nq, off);
+    }
     HIP_OK(c->seed_off.upload(off.data(), off.size()));
     HIP_OK(c->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
     return run_search(ix, c, prm, d_queries, query_bytes, nq, c->seeds.p, c->seed_off.p, d_ids,
@@ -463,11 +525,18 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
                     d_n, d_counters, s);
 }
 
+extern "C" uint32_t ngt_amd_last_search_slots(const ngt_amd_index* ix) {
+  if (!ix) return 0;
+  SearchCtx* c = ix->last_ctx.load();
+  return c ? c->launch_slots : 0;
+}
+
 extern "C" float ngt_amd_last_search_kernel_ms(const ngt_amd_index* ix) {
   if (!ix) return 0.f;
-  if (!ix->last_ctx) return -1.f;
+  SearchCtx* c = ix->last_ctx.load();
+  if (!c) return -1.f;
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, ix->last_ctx->ev0, ix->last_ctx->ev1) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.f;
   return ms;
 }
 
@@ -476,7 +545,7 @@ int ngt_amd::upload_queries(ngt_amd_index* ix, const void* queries, uint32_t nq,
                           DevBuf<uint8_t>& prep, hipStream_t s) {
   // host queries are float [nq][dim] for every object type (Index::allocateObject
   // converts them to the object type, ObjectRepository.h:222-253)
-  HIP_OK(raw.upload(static_cast<const float*>(queries), (size_t)nq * ix->dim));
+  HIP_OK(raw.upload_async(static_cast<const float*>(queries), (size_t)nq * ix->dim, s));
   HIP_OK(prep.alloc((size_t)nq * ix->row_bytes));
   if (ngt_amd_prepare_queries_device(ix, raw.p, nq, prep.p, s)) return -1;
   return 0;
@@ -487,8 +556,10 @@ extern "C" int ngt_amd_prepare_queries_device(ngt_amd_index* ix, const float* d_
   if (!ix || (!d_in && nq) || (!d_out && nq)) return fail("ngt_amd_prepare_queries_device: bad arguments");
   if (nq == 0) return 0;
   hipStream_t s = (hipStream_t)stream;  // null = the default stream
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
   bool normalize = ix->metric == 5 || ix->metric == 6 || ix->metric == 9;
-  HIP_OK(launch_prepare_queries(d_in, ix->dim, nq, ix->dp, ix->otype, normalize, d_out, ix->error.p, s));
+  HIP_OK(launch_prepare_queries(d_in, ix->dim, nq, ix->dp, ix->otype, normalize, d_out, c->err.p, s));
   return 0;
 }
 
@@ -497,45 +568,43 @@ extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* pr
                               uint32_t* ids, float* dists, uint32_t* n, uint64_t* counters) {
   if (!ix || !prm || (!queries && nq) || !ids || !dists || !n) return fail("ngt_amd_search: bad arguments");
   if (nq == 0) return 0;
-  HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = ix->stream;
-  DevBuf<float> raw;
-  DevBuf<uint8_t> q;
-  if (upload_queries(ix, queries, nq, raw, q, s)) return -1;
-  DevBuf<uint32_t> d_ids, d_n, d_seeds;
-  DevBuf<float> d_dists;
-  DevBuf<uint64_t> d_cnt, d_seed_off;
-  HIP_OK(d_ids.alloc((size_t)nq * prm->k));
-  HIP_OK(d_dists.alloc((size_t)nq * prm->k));
-  HIP_OK(d_n.alloc(nq));
-  if (counters) HIP_OK(d_cnt.alloc((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY));
-  const uint32_t* sp = nullptr;
-  const uint64_t* so = nullptr;
   if (prm->seed_mode == NGT_AMD_SEED_GIVEN) {
     if (!seeds || !seed_off) return fail("ngt_amd_search: NGT_AMD_SEED_GIVEN needs seeds and seed_off");
     for (uint64_t i = 0; i < seed_off[nq]; i++)
       if (seeds[i] == 0 || seeds[i] >= ix->nrows) return fail("ngt_amd_search: seed id %u out of range", seeds[i]);
-    HIP_OK(d_seeds.upload(seeds, seed_off[nq]));
-    HIP_OK(d_seed_off.upload(seed_off, (size_t)nq + 1));
-    sp = d_seeds.p;
-    so = d_seed_off.p;
   }
-  if (ngt_amd_search_device(ix, prm, q.p, ix->row_bytes, nq, sp, so, d_ids.p, d_dists.p, d_n.p,
-                            counters ? d_cnt.p : nullptr, s))
+  HIP_OK(hipSetDevice(ix->device));
+  CallGuard g(ix);
+  CallCtx* cc = g.c;
+  if (!cc) return -1;
+  hipStream_t s = cc->stream;
+  if (upload_queries(ix, queries, nq, cc->raw, cc->prep, s)) return -1;
+  HIP_OK(cc->ids.alloc((size_t)nq * prm->k));
+  HIP_OK(cc->dists.alloc((size_t)nq * prm->k));
+  HIP_OK(cc->n.alloc(nq));
+  if (counters) HIP_OK(cc->cnt.alloc((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY));
+  const uint32_t* sp = nullptr;
+  const uint64_t* so = nullptr;
+  if (prm->seed_mode == NGT_AMD_SEED_GIVEN) {
+    HIP_OK(cc->seeds.alloc(std::max<uint64_t>(seed_off[nq], 1)));
+    HIP_OK(cc->seed_off.alloc((size_t)nq + 1));
+    HIP_OK(hipMemcpyAsync(cc->seeds.p, seeds, seed_off[nq] * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(cc->seed_off.p, seed_off, ((size_t)nq + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    sp = cc->seeds.p;
+    so = cc->seed_off.p;
+  }
+  if (ngt_amd_search_device(ix, prm, cc->prep.p, ix->row_bytes, nq, sp, so, cc->ids.p, cc->dists.p, cc->n.p,
+                            counters ? cc->cnt.p : nullptr, s))
     return -1;
-  HIP_OK(hipMemcpyAsync(ids, d_ids.p, (size_t)nq * prm->k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(dists, d_dists.p, (size_t)nq * prm->k * sizeof(float), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(n, d_n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(ids, cc->ids.p, (size_t)nq * prm->k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(dists, cc->dists.p, (size_t)nq * prm->k * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(n, cc->n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (counters)
-    HIP_OK(hipMemcpyAsync(counters, d_cnt.p, (size_t)nq * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
+    HIP_OK(hipMemcpyAsync(counters, cc->cnt.p, (size_t)nq * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
                           hipMemcpyDeviceToHost, s));
   int herr = 0;
-  HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
-  if (herr) {
-    (void)hipMemset(ix->error.p, 0, sizeof(int));
-    return fail("ngt_amd_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
-  }
+  if (take_device_error(ix, s, &herr)) return -1;
+  if (herr) return fail("ngt_amd_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
   return 0;
 }
 
@@ -550,7 +619,9 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
   uint64_t want = ((uint64_t)ix->cu_count * 16 + nq - 1) / nq;
   uint64_t maxs = (ix->nrows + 255) / 256;
   uint32_t nslices = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxs, 1)));
-  static thread_local DevBuf<uint64_t> partial;
+  SearchCtx* c = ctx_for(ix, s);  // the slice buffer belongs to this index and stream
+  if (!c) return -1;
+  DevBuf<uint64_t>& partial = c->partial;
   HIP_OK(partial.alloc((size_t)nq * nslices * k));
   LinearArgs a{};
   a.rows = ix->rows.p;
@@ -576,20 +647,19 @@ extern "C" int ngt_amd_linear_search(ngt_amd_index* ix, const void* queries, uin
   if (!ix || (!queries && nq) || !ids || !dists || !n || k == 0) return fail("ngt_amd_linear_search: bad arguments");
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = ix->stream;
-  DevBuf<float> raw;
-  DevBuf<uint8_t> q;
-  if (upload_queries(ix, queries, nq, raw, q, s)) return -1;
-  DevBuf<uint32_t> d_ids, d_n;
-  DevBuf<float> d_dists;
-  HIP_OK(d_ids.alloc((size_t)nq * k));
-  HIP_OK(d_dists.alloc((size_t)nq * k));
-  HIP_OK(d_n.alloc(nq));
-  if (ngt_amd_linear_search_device(ix, q.p, ix->row_bytes, nq, k, radius, d_ids.p, d_dists.p, d_n.p, s))
+  CallGuard g(ix);
+  CallCtx* cc = g.c;
+  if (!cc) return -1;
+  hipStream_t s = cc->stream;
+  if (upload_queries(ix, queries, nq, cc->raw, cc->prep, s)) return -1;
+  HIP_OK(cc->ids.alloc((size_t)nq * k));
+  HIP_OK(cc->dists.alloc((size_t)nq * k));
+  HIP_OK(cc->n.alloc(nq));
+  if (ngt_amd_linear_search_device(ix, cc->prep.p, ix->row_bytes, nq, k, radius, cc->ids.p, cc->dists.p, cc->n.p, s))
     return -1;
-  HIP_OK(hipMemcpyAsync(ids, d_ids.p, (size_t)nq * k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(dists, d_dists.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(n, d_n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(ids, cc->ids.p, (size_t)nq * k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(dists, cc->dists.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(n, cc->n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   return 0;
 }
@@ -605,7 +675,9 @@ extern "C" int ngt_amd_distances(ngt_amd_index* ix, const void* queries, uint32_
     if (qidx[i] >= nq) return fail("ngt_amd_distances: query index %u out of range", qidx[i]);
     if (oid[i] >= ix->nrows) return fail("ngt_amd_distances: object id %u out of range", oid[i]);
   }
-  hipStream_t s = ix->stream;
+  CallGuard g(ix);
+  if (!g.c) return -1;
+  hipStream_t s = g.c->stream;
   DevBuf<uint8_t> q;
   HIP_OK(q.upload(static_cast<const uint8_t*>(queries), (size_t)nq * ix->row_bytes));
   DevBuf<uint32_t> dq, dobj;

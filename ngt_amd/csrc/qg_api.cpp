@@ -234,13 +234,13 @@ extern "C" int ngt_amd_qg_lut(ngt_amd_index* ix, const float* queries, uint32_t 
   if (!ix->qg.ready) return fail("ngt_amd_qg_lut: the index has no quantizer");
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = ix->stream;
-  DevBuf<float> raw;
-  DevBuf<uint8_t> prep;
-  if (upload_queries(ix, queries, nq, raw, prep, s)) return -1;
+  CallGuard g(ix);
+  if (!g.c) return -1;
+  hipStream_t s = g.c->stream;
+  if (upload_queries(ix, queries, nq, g.c->raw, g.c->prep, s)) return -1;
   SearchCtx* c = ctx_for(ix, s);
   if (!c) return -1;
-  if (run_lut(ix, c, prep.p, ix->row_bytes, nq, s)) return -1;
+  if (run_lut(ix, c, g.c->prep.p, ix->row_bytes, nq, s)) return -1;
   const QgState& q = ix->qg;
   HIP_OK(hipMemcpyAsync(lut, c->lut.p, (size_t)nq * q.Me * 16, hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(scale, c->scale.p, nq * sizeof(float), hipMemcpyDeviceToHost, s));
@@ -261,7 +261,9 @@ extern "C" int ngt_amd_qg_adc(ngt_amd_index* ix, const uint8_t* lut, const float
     if (node[i] >= ix->nrows) return fail("ngt_amd_qg_adc: node %u out of range", node[i]);
   }
   HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = ix->stream;
+  CallGuard g(ix);
+  if (!g.c) return -1;
+  hipStream_t s = g.c->stream;
   const QgState& q = ix->qg;
   DevBuf<uint8_t> dl;
   DevBuf<float> dsc, dto, dout;
@@ -358,7 +360,7 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   a.out_dists = d_dists;
   a.out_n = d_n;
   a.counters = d_counters;
-  a.error = ix->error.p;
+  a.error = c->err.p;
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
     // getSeedsFromTree with the caller's k (before the expansion, :362)
@@ -368,7 +370,11 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
     a.seed_count = c->seed_count.p;
   } else if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
-    std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
+    std::vector<uint32_t> seeds;
+    {
+      std::lock_guard<std::mutex> lk(ix->mu);  // one query after another on the rand() stream
+      seeds = random_seed_lists(ix, nq, off);
+    }
     HIP_OK(c->seed_off.upload(off.data(), off.size()));
     HIP_OK(c->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
     a.seeds = c->seeds.p;
@@ -387,7 +393,7 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   const size_t lds = qg_search_lds_bytes(a);
   if (lds > 64 * 1024)
     return fail("ngt_amd_qg_search: k=%u x expansion needs %zu bytes of LDS per query (max 65536)", a.k, lds);
-  if (ensure_vis_scratch(ix, c, lds, s)) return -1;
+  if (ensure_vis_scratch(ix, c, lds, nq, s)) return -1;
   a.vis = c->vis.p;
   a.vis_stride = c->vis_stride;
   a.slot_epoch = c->slot_epoch.p;
@@ -396,6 +402,7 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   a.work = c->work.p;
   HIP_OK(hipMemsetAsync(c->work.p, 0, sizeof(uint32_t), s));
   const uint32_t slots = std::min<uint32_t>(c->slots, nq);
+  c->launch_slots = slots;
   HIP_OK(hipEventRecord(c->ev0, s));
   HIP_OK(launch_qg_search(a, slots, s));
   HIP_OK(hipEventRecord(c->ev1, s));
@@ -407,44 +414,42 @@ extern "C" int ngt_amd_qg_search(ngt_amd_index* ix, const ngt_amd_qg_search_para
                                  float* dists, uint32_t* n, uint64_t* counters) {
   if (!ix || !prm || (!queries && nq) || !ids || !dists || !n) return fail("ngt_amd_qg_search: bad arguments");
   if (nq == 0) return 0;
-  HIP_OK(hipSetDevice(ix->device));
-  hipStream_t s = ix->stream;
-  DevBuf<float> raw;
-  DevBuf<uint8_t> qb;
-  if (upload_queries(ix, queries, nq, raw, qb, s)) return -1;
-  DevBuf<uint32_t> d_ids, d_n, d_seeds;
-  DevBuf<float> d_dists;
-  DevBuf<uint64_t> d_cnt, d_seed_off;
-  HIP_OK(d_ids.alloc((size_t)nq * prm->k));
-  HIP_OK(d_dists.alloc((size_t)nq * prm->k));
-  HIP_OK(d_n.alloc(nq));
-  if (counters) HIP_OK(d_cnt.alloc((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY));
-  const uint32_t* sp = nullptr;
-  const uint64_t* so = nullptr;
   if (prm->seed_mode == NGT_AMD_SEED_GIVEN) {
     if (!seeds || !seed_off) return fail("ngt_amd_qg_search: NGT_AMD_SEED_GIVEN needs seeds and seed_off");
     for (uint64_t i = 0; i < seed_off[nq]; i++)
       if (seeds[i] == 0 || seeds[i] >= ix->nrows) return fail("ngt_amd_qg_search: seed id %u out of range", seeds[i]);
-    HIP_OK(d_seeds.upload(seeds, std::max<uint64_t>(seed_off[nq], 1)));
-    HIP_OK(d_seed_off.upload(seed_off, (size_t)nq + 1));
-    sp = d_seeds.p;
-    so = d_seed_off.p;
   }
-  if (ngt_amd_qg_search_device(ix, prm, qb.p, ix->row_bytes, nq, sp, so, d_ids.p, d_dists.p, d_n.p,
-                               counters ? d_cnt.p : nullptr, s))
+  HIP_OK(hipSetDevice(ix->device));
+  CallGuard g(ix);
+  CallCtx* cc = g.c;
+  if (!cc) return -1;
+  hipStream_t s = cc->stream;
+  if (upload_queries(ix, queries, nq, cc->raw, cc->prep, s)) return -1;
+  HIP_OK(cc->ids.alloc((size_t)nq * prm->k));
+  HIP_OK(cc->dists.alloc((size_t)nq * prm->k));
+  HIP_OK(cc->n.alloc(nq));
+  if (counters) HIP_OK(cc->cnt.alloc((size_t)nq * NGT_AMD_COUNTERS_PER_QUERY));
+  const uint32_t* sp = nullptr;
+  const uint64_t* so = nullptr;
+  if (prm->seed_mode == NGT_AMD_SEED_GIVEN) {
+    HIP_OK(cc->seeds.alloc(std::max<uint64_t>(seed_off[nq], 1)));
+    HIP_OK(cc->seed_off.alloc((size_t)nq + 1));
+    HIP_OK(hipMemcpyAsync(cc->seeds.p, seeds, seed_off[nq] * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(cc->seed_off.p, seed_off, ((size_t)nq + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    sp = cc->seeds.p;
+    so = cc->seed_off.p;
+  }
+  if (ngt_amd_qg_search_device(ix, prm, cc->prep.p, ix->row_bytes, nq, sp, so, cc->ids.p, cc->dists.p, cc->n.p,
+                               counters ? cc->cnt.p : nullptr, s))
     return -1;
-  HIP_OK(hipMemcpyAsync(ids, d_ids.p, (size_t)nq * prm->k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(dists, d_dists.p, (size_t)nq * prm->k * sizeof(float), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(n, d_n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(ids, cc->ids.p, (size_t)nq * prm->k * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(dists, cc->dists.p, (size_t)nq * prm->k * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(n, cc->n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (counters)
-    HIP_OK(hipMemcpyAsync(counters, d_cnt.p, (size_t)nq * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
+    HIP_OK(hipMemcpyAsync(counters, cc->cnt.p, (size_t)nq * NGT_AMD_COUNTERS_PER_QUERY * sizeof(uint64_t),
                           hipMemcpyDeviceToHost, s));
   int herr = 0;
-  HIP_OK(hipMemcpyAsync(&herr, ix->error.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
-  if (herr) {
-    (void)hipMemset(ix->error.p, 0, sizeof(int));
-    return fail("ngt_amd_qg_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
-  }
+  if (take_device_error(ix, s, &herr)) return -1;
+  if (herr) return fail("ngt_amd_qg_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
   return 0;
 }

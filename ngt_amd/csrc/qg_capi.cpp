@@ -13,6 +13,7 @@
 #include <fstream>
 
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -20,6 +21,7 @@
 #include "../../include/NGT/Capi.h"
 #include "../../include/NGT/NGTQ/Capi.h"
 #include "../../include/ngt_amd.h"
+#include "coalesce.h"
 #include "index_io.h"
 
 namespace {
@@ -28,6 +30,7 @@ struct QgCapiIndex {
   ngt_amd::HostIndex host;
   ngt_amd::HostQuantizer quant;
   ngt_amd_index* dev = nullptr;
+  std::unique_ptr<ngt_amd::Coalescer> co;  // concurrent ngtqg_search_index callers
   ~QgCapiIndex() {
     if (dev) ngt_amd_index_destroy(dev);
   }
@@ -212,6 +215,7 @@ NGTQGIndex ngtqg_open_index(const char* index_path, NGTError error) {
     delete ix;
     return NULL;
   }
+  ix->co.reset(new ngt_amd::Coalescer((uint32_t)ix->host.prop.dimension));
   return static_cast<NGTQGIndex>(ix);
 }
 
@@ -295,17 +299,48 @@ bool ngtqg_search_index(NGTQGIndex index, NGTQGQuery query, NGTObjectDistances r
   }
   auto* ix = static_cast<QgCapiIndex*>(index);
   if (query.radius < 0.0) query.radius = FLT_MAX;
-  std::vector<uint32_t> ids, n;
+  std::vector<uint32_t> ids;
   std::vector<float> dists;
-  std::string e = run(ix, query.query, 1, query.size, query.epsilon, query.result_expansion, query.radius, ids,
-                      dists, n);
+  uint32_t nres = 0;
+  std::string e;
+  if (!ngt_amd::coalesce_enabled()) {
+    std::vector<uint32_t> n;
+    e = run(ix, query.query, 1, query.size, query.epsilon, query.result_expansion, query.radius, ids, dists, n);
+    nres = n.empty() ? 0 : n[0];
+  } else {
+    // concurrent callers with equal parameters share one launch (coalesce.h)
+    ngt_amd::CoalesceReq r;
+    r.key.kind = 2;
+    r.key.size = (uint32_t)query.size;
+    r.key.epsilon = query.epsilon;
+    r.key.radius = query.radius;
+    r.key.expansion = query.result_expansion;
+    r.query = query.query;
+    ix->co->submit(&r, [ix](const ngt_amd::CoalesceKey& k, const float* qs, uint32_t nq,
+                            std::vector<ngt_amd::CoalesceReq*>& batch) {
+      std::vector<uint32_t> vi, vn;
+      std::vector<float> vd;
+      std::string err = run(ix, qs, nq, k.size, k.epsilon, k.expansion, k.radius, vi, vd, vn);
+      for (uint32_t i = 0; i < nq; i++) {
+        batch[i]->err = err;
+        if (!err.empty()) continue;
+        batch[i]->n = vn[i];
+        batch[i]->ids.assign(vi.begin() + (size_t)i * k.size, vi.begin() + (size_t)i * k.size + vn[i]);
+        batch[i]->dists.assign(vd.begin() + (size_t)i * k.size, vd.begin() + (size_t)i * k.size + vn[i]);
+      }
+    });
+    e = r.err;
+    ids.swap(r.ids);
+    dists.swap(r.dists);
+    nres = r.n;
+  }
   if (!e.empty()) {
     report(error, std::string("Capi : ") + __FUNCTION__ + "() : Error: " + e);
     return false;
   }
   Results* r = static_cast<Results*>(results);
   r->clear();  // moveFrom overwrites the result set
-  for (uint32_t i = 0; i < n[0]; i++) r->push_back(NGTObjectDistance{ids[i], dists[i]});
+  for (uint32_t i = 0; i < nres; i++) r->push_back(NGTObjectDistance{ids[i], dists[i]});
   return true;
 }
 

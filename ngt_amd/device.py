@@ -127,6 +127,10 @@ class DeviceIndex(object):
     def last_search_kernel_ms(self):
         return float(self.L.ngt_amd_last_search_kernel_ms(self.h))
 
+    def last_search_slots(self):
+        """Workgroups (resident query slots) of the last search launch."""
+        return int(self.L.ngt_amd_last_search_slots(self.h))
+
     def prepare_queries_device(self, d_in, nq, d_out, stream=None):
         _chk(self.L.ngt_amd_prepare_queries_device(self.h, d_in, nq, d_out, stream))
 

@@ -23,8 +23,8 @@ def create(path, dimension, edge_size_for_creation=10, edge_size_for_search=40, 
     ot = {"Float": "Float", "float": "Float", "Byte": "Integer", "byte": "Integer"}.get(object_type)
     if ot is None:
         raise NativeError("ngtpy::create: invalid object type. " + object_type)
-    if distance_type not in ("L1", "L2", "Hamming", "Jaccard", "Angle", "Normalized Angle", "Cosine",
-                             "Normalized Cosine"):
+    if distance_type not in ("L1", "L2", "Normalized L2", "Hamming", "Jaccard", "Sparse Jaccard", "Angle",
+                             "Normalized Angle", "Cosine", "Normalized Cosine"):
         raise NativeError("ngtpy::create: invalid distance type. " + distance_type)
     base.Index.create(path, dimension, edge_size_for_creation, edge_size_for_search, ot, distance_type)
 
@@ -72,10 +72,13 @@ class Index(object):
         return self._results(ids, ds, n, with_distance)
 
     def linear_search(self, query, size=0, with_distance=True):
-        """ngtpy.cpp:216-268: exact k-NN by full scan."""
+        """ngtpy.cpp:216-268: exact k-NN by full scan within the index's search
+        radius (sc.setRadius(defaultRadius)).  The reference adds
+        sc.distanceComputationCount, which ObjectSpaceRepository::linearSearch
+        (ObjectSpaceRepository.h:466-502) never increments: the count is unchanged."""
         q = np.ascontiguousarray(query, dtype=np.float32).reshape(1, -1)
         k = size if size > 0 else self.num_of_search_objects
-        ids, ds, n = self._ix.batch_linear_search(q, k)
+        ids, ds, n = self._ix.batch_linear_search(q, k, radius=self.radius)
         return self._results(ids, ds, n, with_distance)
 
     def get_num_of_distance_computations(self):
@@ -113,6 +116,9 @@ class Index(object):
         return [float(x) for x in self._ix.get_object(self._id_in(object_id))]
 
     def remove(self, object_id):
+        """Not supported: GraphAndTreeIndex::remove re-links the graph around the
+        removed node (graph maintenance, out of this build's scope); raises
+        NativeError with the C API's message."""
         L = self._ix._L
         self._ix._check(L.ngt_remove_index(self._ix.index, self._id_in(object_id), self._ix.err), self._ix.err)
 

@@ -275,10 +275,20 @@ void ngto_distances(int metric, int otype, const void *query, const void *rows,
                            (const uint8_t *)rows + (size_t)ids[i] * row_bytes, dp);
 }
 
-/* ObjectSpace::normalize<float> (ObjectSpace.h:251-266). */
+/* ObjectSpace::normalize<float> (ObjectSpace.h:251-266) as the reference's
+ * -Ofast AVX-512 build vectorizes the sum: 16 FMA lanes over the unpadded
+ * dimension, folded 8/4/2/1, then a sequential FMA tail.  The reference then
+ * scales by vrsqrtss + one Newton step (host-CPU-dependent bits, so parity is
+ * within 2 ulp, tests/golden/norm_f_d*.npz); this restatement -- like the
+ * device preparation -- takes sqrtf and divides. */
 int ngto_normalize_f32(float *v, size_t dim) {
-  float sum = 0.0f;
-  for (size_t i = 0; i < dim; i++) sum += v[i] * v[i];
+  float acc[16] = {0};
+  const size_t main = dim & ~(size_t)15;
+  for (size_t i = 0; i < main; i++) acc[i & 15] = fmaf(v[i], v[i], acc[i & 15]);
+  for (int w = 8; w >= 1; w >>= 1)
+    for (int l = 0; l < w; l++) acc[l] = acc[l + w] + acc[l];
+  float sum = acc[0];
+  for (size_t i = main; i < dim; i++) sum = fmaf(v[i], v[i], sum);
   if (sum == 0.0f) return -1;
   sum = sqrtf(sum);
   for (size_t i = 0; i < dim; i++) v[i] = v[i] / sum;
@@ -696,4 +706,67 @@ int ngto_qg_search(const float *rows, size_t dp, size_t nrows, const uint64_t *q
     counters[3] = nexact;
   }
   return n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Query batches, one query per thread -- the CPU baseline bench.py times and */
+/* the parity sample it checks the device against.  Each query is the single- */
+/* query function above, so results do not depend on the thread count.        */
+/* ------------------------------------------------------------------------- */
+
+void ngto_search_batch(int metric, int otype, const void *rows, size_t row_bytes, size_t nrows, size_t dp,
+                       const uint64_t *edge_off, const uint32_t *edge_ids, const void *queries,
+                       size_t query_bytes, size_t nq, const uint32_t *seeds, const uint64_t *seed_off, size_t k,
+                       float epsilon, float radius, size_t edge_size, uint32_t *out_ids, float *out_dists,
+                       uint32_t *out_n, uint64_t *counters, int nthreads) {
+  long q;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+  for (q = 0; q < (long)nq; q++) {
+    uint64_t c[3] = {0, 0, 0};
+    int n = ngto_search(metric, otype, rows, row_bytes, nrows, dp, edge_off, edge_ids,
+                        (const uint8_t *)queries + (size_t)q * query_bytes, seeds + seed_off[q],
+                        (size_t)(seed_off[q + 1] - seed_off[q]), k, epsilon, radius, edge_size,
+                        out_ids + (size_t)q * k, out_dists + (size_t)q * k, c);
+    out_n[q] = (uint32_t)n;
+    if (counters) memcpy(counters + 3 * (size_t)q, c, sizeof c);
+  }
+  (void)nthreads;
+}
+
+void ngto_linear_search_batch(int metric, int otype, const void *rows, size_t row_bytes, size_t nrows, size_t dp,
+                              const void *queries, size_t query_bytes, size_t nq, size_t k, double radius,
+                              uint32_t *out_ids, float *out_dists, uint32_t *out_n, int nthreads) {
+  long q;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+  for (q = 0; q < (long)nq; q++)
+    out_n[q] = (uint32_t)ngto_linear_search(metric, otype, rows, row_bytes, nrows, dp, NULL,
+                                            (const uint8_t *)queries + (size_t)q * query_bytes, k, radius,
+                                            out_ids + (size_t)q * k, out_dists + (size_t)q * k);
+  (void)nthreads;
+}
+
+void ngto_qg_search_batch(const float *rows, size_t dp, size_t nrows, const uint64_t *qoff, const uint32_t *qids,
+                          const uint64_t *code_off, const uint8_t *codes, size_t M, const uint8_t *luts,
+                          size_t lut_stride, const float *scales, const float *offsets, const float *queries,
+                          size_t nq, const uint32_t *seeds, const uint64_t *seed_off, size_t k, float epsilon,
+                          float result_expansion, float radius, size_t out_stride, uint32_t *out_ids,
+                          float *out_dists, uint32_t *out_n, uint64_t *counters, int nthreads) {
+  long q;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+  for (q = 0; q < (long)nq; q++) {
+    uint64_t c[4] = {0, 0, 0, 0};
+    int n = ngto_qg_search(rows, dp, nrows, qoff, qids, code_off, codes, M, luts + (size_t)q * lut_stride,
+                           scales[q], offsets[q], queries + (size_t)q * dp, seeds + seed_off[q],
+                           (size_t)(seed_off[q + 1] - seed_off[q]), k, epsilon, result_expansion, radius,
+                           out_ids + (size_t)q * out_stride, out_dists + (size_t)q * out_stride, c);
+    out_n[q] = (uint32_t)n;
+    if (counters) memcpy(counters + 4 * (size_t)q, c, sizeof c);
+  }
+  (void)nthreads;
 }

@@ -122,6 +122,27 @@ int ngto_qg_search(const float *rows, size_t dp, size_t nrows, const uint64_t *q
                    float result_expansion, float radius, uint32_t *out_ids, float *out_dists,
                    uint64_t *counters);
 
+/* ---- query batches, one query per thread (OpenMP builds; bench.py's
+ * cpu_baseline and parity sample).  Per query exactly the single-query
+ * function above: ngto_search (ids/dists [nq][k], n [nq], counters [nq][3]),
+ * ngto_linear_search, ngto_qg_search (outputs [nq][out_stride], counters
+ * [nq][4]; luts [nq][lut_stride]).  Queries are padded rows query_bytes
+ * apart (QG: dp floats apart); seeds CSR: seeds[seed_off[q] .. seed_off[q+1]). */
+void ngto_search_batch(int metric, int otype, const void *rows, size_t row_bytes, size_t nrows, size_t dp,
+                       const uint64_t *edge_off, const uint32_t *edge_ids, const void *queries,
+                       size_t query_bytes, size_t nq, const uint32_t *seeds, const uint64_t *seed_off, size_t k,
+                       float epsilon, float radius, size_t edge_size, uint32_t *out_ids, float *out_dists,
+                       uint32_t *out_n, uint64_t *counters, int nthreads);
+void ngto_linear_search_batch(int metric, int otype, const void *rows, size_t row_bytes, size_t nrows, size_t dp,
+                              const void *queries, size_t query_bytes, size_t nq, size_t k, double radius,
+                              uint32_t *out_ids, float *out_dists, uint32_t *out_n, int nthreads);
+void ngto_qg_search_batch(const float *rows, size_t dp, size_t nrows, const uint64_t *qoff, const uint32_t *qids,
+                          const uint64_t *code_off, const uint8_t *codes, size_t M, const uint8_t *luts,
+                          size_t lut_stride, const float *scales, const float *offsets, const float *queries,
+                          size_t nq, const uint32_t *seeds, const uint64_t *seed_off, size_t k, float epsilon,
+                          float result_expansion, float radius, size_t out_stride, uint32_t *out_ids,
+                          float *out_dists, uint32_t *out_n, uint64_t *counters, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

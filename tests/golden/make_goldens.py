@@ -3,11 +3,14 @@
 
 Run in the development container only (never on the GPU box):
 
-    python3 tests/golden/make_goldens.py --ngt /tmp/ngt-build/bin/ngt/ngt \
-        --lib /tmp/ngt-build/lib/NGT --ref /root/reference --out tests/golden
+    make -f oracle/ref.mk                      # the reference, built from its sources
+    python3 tests/golden/make_goldens.py --out tests/golden
 
-The `ngt` binary is the reference built from /root/reference during the
-survey (out-of-tree, /tmp/ngt-build); this script only *runs* it.  It writes:
+The `ngt` binary is the reference built from /root/reference by the committed
+recipe oracle/ref.mk into oracle/_ref/; this script only *runs* it.
+``--subset quick`` regenerates only the C1 ANNG, its tree-seeded searches at
+epsilon 0.1 and two comparator fixtures (what tests/test_golden_regen.py
+compares against the committed files).  It writes:
 
 * ``c1_anng/``   -- the reference-built index for BASELINE config 1
   (``ngt create -d 128 -o f -D 2`` on data/sift-dataset-5k.tsv): prf/obj/grp/tre
@@ -49,8 +52,10 @@ def write_tsv(path, a, fmt):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ngt", default="/tmp/ngt-build/bin/ngt/ngt")
-    ap.add_argument("--lib", default="/tmp/ngt-build/lib/NGT")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    ap.add_argument("--ngt", default=os.path.join(root, "oracle", "_ref", "ngt"))
+    ap.add_argument("--lib", default=os.path.join(root, "oracle", "_ref"))
+    ap.add_argument("--subset", choices=["all", "quick"], default="all")
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.dirname(os.path.abspath(__file__)))
     ap.add_argument("--work", default="/tmp/ngt_goldens")
@@ -75,19 +80,21 @@ def main():
     write_tsv(os.path.join(work, "sift5k.tsv"), sift, "%d")
     write_tsv(os.path.join(work, "q100.tsv"), queries, "%d")
 
+    quick = args.subset == "quick"
     # ---- C1: ANNG on sift-5k (BASELINE config 1) ---------------------------
     run([ngt, "create", "-d", "128", "-o", "f", "-D", "2", "c1_anng", "sift5k.tsv"], env, work)
     # ---- ONNG on sift-5k ---------------------------------------------------
-    run([ngt, "create", "-i", "t", "-g", "a", "-S", "0", "-e", "0.1", "-E", "100",
-         "-d", "128", "-o", "f", "-D", "2", "anng100", "sift5k.tsv"], env, work)
-    run([ngt, "reconstruct-graph", "-m", "S", "-o", "10", "-i", "120", "anng100", "c1_onng"], env, work)
+    if not quick:
+        run([ngt, "create", "-i", "t", "-g", "a", "-S", "0", "-e", "0.1", "-E", "100",
+             "-d", "128", "-o", "f", "-D", "2", "anng100", "sift5k.tsv"], env, work)
+        run([ngt, "reconstruct-graph", "-m", "S", "-o", "10", "-i", "120", "anng100", "c1_onng"], env, work)
 
-    for name in ["c1_anng", "c1_onng"]:
+    for name in (["c1_anng"] if quick else ["c1_anng", "c1_onng"]):
         dst = os.path.join(args.out, name)
         shutil.rmtree(dst, ignore_errors=True)
         shutil.copytree(os.path.join(work, name), dst)
-        for mode in ["t", "g", "s"]:
-            for eps in (EPSILONS if mode != "s" else ["0.0"]):
+        for mode in (["t"] if quick else ["t", "g", "s"]):
+            for eps in (["0.1"] if quick else EPSILONS if mode != "s" else ["0.0"]):
                 for om in (["r", "w"] if mode != "s" else ["r"]):
                     txt = run([ngt, "search", "-i", mode, "-n", "10", "-e", eps, "-m", om,
                                "-o", "e", name, "q100.tsv"], env, work)
@@ -103,6 +110,8 @@ def main():
                         ids=ids, dists=dists,
                         ndist=np.array([r["ndist"] for r in res]),
                         nvisit=np.array([r["nvisit"] for r in res]))
+        if quick:
+            continue
         # k=20 with a larger epsilon exercises a longer traversal.
         txt = run([ngt, "search", "-i", "t", "-n", "20", "-e", "0.2", "-o", "e", name, "q100.tsv"], env, work)
         res = ngt_files.parse_search_output(txt)
@@ -122,6 +131,8 @@ def main():
         ("h", "hamming", "c", 128), ("h", "hamming", "c", 100), ("j", "jaccard", "c", 128),
         ("c", "cosine", "c", 128), ("a", "angle", "c", 100),
     ]
+    if quick:
+        specs = [("2", "l2", "f", 128), ("h", "hamming", "c", 128)]
     for flag, mname, ot, dim in specs:
         data = sub[:, :dim]
         if ot == "f":
@@ -142,6 +153,8 @@ def main():
                             rows=rows, src=src, dst=ids, dist=dists, dim=dim)
         print(mname, ot, dim, "pairs", len(ids))
 
+    if quick:
+        return
     # Poincare / Lorentz sets shipped with the reference (first 400 rows).
     for flag, mname, fn in [("p", "poincare", "poincare-input-5k.tsv"), ("l", "lorentz", "lorentz-input-5k.tsv")]:
         data = np.loadtxt(os.path.join(args.ref, "data", fn), delimiter="\t")[:400]

@@ -3,15 +3,17 @@
 
 Development container only (never on the GPU box):
 
+    make -f oracle/ref.mk                      # the reference, built from its sources
     python3 tests/golden/make_qg_goldens.py
 
-Steps (all reference binaries come from the out-of-tree build /tmp/ngt-build):
+Steps (all reference binaries come from oracle/_ref/, built from
+/root/reference by the committed recipe oracle/ref.mk):
 
 1. ``ngtqg quantize -E 128`` on a copy of ``c1_onng`` (ONNG over SIFT-5k,
    dsub=1 => M=128 subspaces), and on a small synthetic ANNG with D=20 and
    ``-Q 4`` (dsub=4 => M=5: odd subspace count + multi-element subvectors).
-2. ``qg_harness.cpp`` (compiled here with the reference's own flags and linked
-   against libngt) records per query the uint8 LUT / scale / totalOffset, ADC
+2. ``qg_harness.cpp`` (compiled by oracle/ref.mk with the reference's own flags
+   and linked against oracle/_ref/libngt_ref.so) records per query the uint8 LUT / scale / totalOffset, ADC
    distances over a few nodes' packed code blocks, and NGTQG::Index::search
    results for several (k, epsilon, result_expansion) triples.
 3. ``ngtqg search`` on the same queries cross-checks the harness's search path
@@ -114,20 +116,20 @@ def keep_state(index, dst):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ngt", default="/tmp/ngt-build/bin/ngt/ngt")
-    ap.add_argument("--ngtqg", default="/tmp/ngt-build/bin/ngtqg/ngtqg")
-    ap.add_argument("--lib", default="/tmp/ngt-build/lib/NGT")
+    ref_out = os.path.join(os.path.dirname(os.path.dirname(HERE)), "oracle", "_ref")
+    ap.add_argument("--ngt", default=os.path.join(ref_out, "ngt"))
+    ap.add_argument("--ngtqg", default=os.path.join(ref_out, "ngtqg"))
+    ap.add_argument("--lib", default=ref_out)
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--work", default="/tmp/ngt_qg_goldens")
-    ap.add_argument("--harness-bin", default="/tmp/ngt_qg_goldens/qg_harness")
+    ap.add_argument("--harness-bin", default=os.path.join(ref_out, "qg_harness"))
     args = ap.parse_args()
     env = dict(os.environ, LD_LIBRARY_PATH=args.lib)
     work = args.work
     shutil.rmtree(work, ignore_errors=True)
     os.makedirs(work)
-    run(["g++", "-fopenmp", "-std=gnu++11", "-Ofast", "-march=native", "-DNDEBUG", "-I" + os.path.join(args.ref, "lib"),
-         "-I" + os.path.join(os.path.dirname(args.lib.rstrip("/")), ""), os.path.join(HERE, "qg_harness.cpp"),
-         "-o", args.harness_bin, "-L" + args.lib, "-lngt", "-lpthread"], env)
+    if not os.path.exists(args.harness_bin):
+        raise SystemExit("build the reference and harnesses first: make -f oracle/ref.mk")
 
     # ---- C1 ONNG, dsub=1 (M=128) -------------------------------------------
     idx = os.path.join(work, "c1")

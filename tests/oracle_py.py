@@ -199,3 +199,113 @@ def qg_search(qg, rows, query, seeds, k, epsilon, expansion, radius=3.402823466e
                          _p(q, ctypes.c_float), _p(seeds, ctypes.c_uint32), len(seeds), k, epsilon, expansion,
                          radius, _p(ids, ctypes.c_uint32), _p(ds, ctypes.c_float), _p(cnt, ctypes.c_uint64))
     return ids[:n].copy(), ds[:n].copy(), cnt
+
+
+# ---------------------------------------------------------------------------
+# Native (vectorized, OpenMP) builds of the same restatement: bench.py's
+# cpu_baseline and parity sample.  x86-64-v4 (AVX-512) when the host has it,
+# else v3 (AVX2).
+# ---------------------------------------------------------------------------
+_NATIVE = {}
+
+
+def host_isa():
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        return "v3"
+    return "v4" if (" avx512f" in flags and " avx512bw" in flags and " avx512vl" in flags
+                    and " avx512dq" in flags) else "v3"
+
+
+def native_lib(isa=None):
+    isa = isa or host_isa()
+    if isa not in _NATIVE:
+        path = os.path.join(ROOT, "oracle", "libngt_oracle_%s.so" % isa)
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(path)
+        vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        f32 = ctypes.c_float
+        L.ngto_search_batch.restype = None
+        L.ngto_search_batch.argtypes = [i32, i32, vp, sz, sz, sz, vp, vp, vp, sz, sz, vp, vp, sz, f32, f32, sz,
+                                        vp, vp, vp, vp, i32]
+        L.ngto_linear_search_batch.restype = None
+        L.ngto_linear_search_batch.argtypes = [i32, i32, vp, sz, sz, sz, vp, sz, sz, sz, ctypes.c_double, vp, vp,
+                                               vp, i32]
+        L.ngto_qg_search_batch.restype = None
+        L.ngto_qg_search_batch.argtypes = [vp, sz, sz, vp, vp, vp, vp, sz, vp, sz, vp, vp, vp, sz, vp, vp, sz, f32,
+                                           f32, f32, sz, vp, vp, vp, vp, i32]
+        _NATIVE[isa] = L
+    return _NATIVE[isa]
+
+
+def search_batch(metric, rows, offsets, edges, queries, seeds, k, epsilon, radius=3.402823466e38, edge_size=0,
+                 threads=1, L=None):
+    """ngto_search over a batch: queries [nq, dp] (rows' dtype), seeds [nq, s]
+    or a list.  Returns ids [nq, k], dists [nq, k], n [nq], counters [nq, 3]."""
+    L = L or native_lib()
+    rows = np.ascontiguousarray(rows)
+    queries = np.ascontiguousarray(queries, dtype=rows.dtype)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    edges = np.ascontiguousarray(edges, dtype=np.uint32)
+    nq = queries.shape[0]
+    if isinstance(seeds, np.ndarray) and seeds.ndim == 2:
+        so = np.arange(nq + 1, dtype=np.uint64) * np.uint64(seeds.shape[1])
+        sp = np.ascontiguousarray(seeds, dtype=np.uint32).reshape(-1)
+    else:
+        so = np.zeros(nq + 1, np.uint64)
+        so[1:] = np.cumsum([len(s) for s in seeds])
+        sp = np.ascontiguousarray(np.concatenate([np.asarray(s, np.uint32) for s in seeds]), dtype=np.uint32)
+    ids = np.zeros((nq, k), np.uint32)
+    ds = np.zeros((nq, k), np.float32)
+    n = np.zeros(nq, np.uint32)
+    cnt = np.zeros((nq, 3), np.uint64)
+    ot = 2 if rows.dtype == np.float32 else 1
+    L.ngto_search_batch(METRICS[metric], ot, rows.ctypes.data, rows.strides[0], rows.shape[0], rows.shape[1],
+                        offsets.ctypes.data, edges.ctypes.data, queries.ctypes.data, queries.strides[0], nq,
+                        sp.ctypes.data, so.ctypes.data, k, epsilon, radius, edge_size, ids.ctypes.data,
+                        ds.ctypes.data, n.ctypes.data, cnt.ctypes.data, threads)
+    return ids, ds, n, cnt
+
+
+def linear_search_batch(metric, rows, queries, k, radius=-1.0, threads=1, L=None):
+    L = L or native_lib()
+    rows = np.ascontiguousarray(rows)
+    queries = np.ascontiguousarray(queries, dtype=rows.dtype)
+    nq = queries.shape[0]
+    ids = np.zeros((nq, k), np.uint32)
+    ds = np.zeros((nq, k), np.float32)
+    n = np.zeros(nq, np.uint32)
+    ot = 2 if rows.dtype == np.float32 else 1
+    L.ngto_linear_search_batch(METRICS[metric], ot, rows.ctypes.data, rows.strides[0], rows.shape[0],
+                               rows.shape[1], queries.ctypes.data, queries.strides[0], nq, k, radius,
+                               ids.ctypes.data, ds.ctypes.data, n.ctypes.data, threads)
+    return ids, ds, n
+
+
+def qg_search_batch(qg, rows, queries, seeds, k, epsilon, expansion, luts, scales, offsets,
+                    radius=3.402823466e38, threads=1, L=None):
+    """ngto_qg_search over a batch (qg: dict of qoff/qids/code_off/codes/M as in
+    qg_search).  Returns ids/dists [nq, stride], n [nq], counters [nq, 4]."""
+    L = L or native_lib()
+    rows = np.ascontiguousarray(rows, dtype=np.float32)
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = queries.shape[0]
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+    so = np.arange(nq + 1, dtype=np.uint64) * np.uint64(seeds.shape[1])
+    stride = max(k, int(k * expansion) + 1)
+    ids = np.zeros((nq, stride), np.uint32)
+    ds = np.zeros((nq, stride), np.float32)
+    n = np.zeros(nq, np.uint32)
+    cnt = np.zeros((nq, 4), np.uint64)
+    luts = np.ascontiguousarray(luts, dtype=np.uint8)
+    scales = np.ascontiguousarray(scales, dtype=np.float32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.float32)
+    L.ngto_qg_search_batch(rows.ctypes.data, rows.shape[1], rows.shape[0], qg["qoff"].ctypes.data,
+                           qg["qids"].ctypes.data, qg["code_off"].ctypes.data, qg["codes"].ctypes.data, qg["M"],
+                           luts.ctypes.data, luts.shape[1], scales.ctypes.data, offsets.ctypes.data,
+                           queries.ctypes.data, nq, seeds.ctypes.data, so.ctypes.data, k, epsilon, expansion,
+                           radius, stride, ids.ctypes.data, ds.ctypes.data, n.ctypes.data, cnt.ctypes.data, threads)
+    return ids, ds, n, cnt

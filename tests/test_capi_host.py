@@ -129,3 +129,20 @@ def test_ngtqg_host_conventions():
     assert "ngtqg_search_index() : parametor error" in L.ngt_get_error_string(err).decode()
     L.ngtqg_close_index(None)
     L.ngt_destroy_error_object(err)
+
+
+def test_wrong_query_length_rejected():
+    """A query whose length is not the index dimension is an error, as
+    allocateObject's check makes it (ObjectRepository.h:228-233), on every
+    search entry point -- raised before any device work."""
+    from ngt_amd import NativeError
+    ix = base.Index(os.path.join(GOLD, "c1_anng"))
+    with pytest.raises(NativeError):
+        ix.batch_search(np.zeros((2, 127), np.float32), 10, 0.1)
+    with pytest.raises(NativeError):
+        ix.batch_linear_search(np.zeros((2, 129), np.float32), 10)
+    with pytest.raises(NativeError, match="dimension"):
+        ix.search(np.zeros(129), 10, 0.1)
+    with pytest.raises(NativeError, match="dimension"):
+        ix.linear_search(np.zeros(100), 10)
+    ix.close()

@@ -187,9 +187,12 @@ def test_search_all_metrics_vs_oracle(path, metric, ot):
         # the oracle sees the query exactly as the device prepared it
         q = np.zeros(rows.shape[1], rows.dtype)
         q[:dim] = qrows[i] if ot == "f" else qrows[i].astype(np.int64).astype(np.uint8)
-        if metric.startswith("normalized"):
-            # normalized queries: same prepared row as the device (see prep_kernels.hip)
-            continue
+        if metric.startswith("normalized") and ot == "f":
+            # ObjectSpace::normalize of the query, restated in the device's
+            # (and the reference's) 16-lane order: the same prepared row
+            qv = np.ascontiguousarray(q[:dim])
+            assert O.lib().ngto_normalize_f32(qv.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), dim) == 0
+            q[:dim] = qv
         oid, od, ocnt = O.search(metric, rows, offs, dst, q, seeds[i], 10, np.float32(0.1))
         assert list(gi[i, :gn[i]]) == list(oid), (i, metric)
         if metric in ("poincare", "lorentz"):

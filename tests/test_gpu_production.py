@@ -1,0 +1,111 @@
+"""The launch configuration the bench times, checked against the oracle.
+
+bench.py times ngt_graph_search_kernel with 16 resident waves per CU, the HBM
+visited epochs behind a 32 Kbit LDS filter and the accepted-only visited set
+(visited_hash_log2 = -2) on a 1M x 128 kNN-derived graph.  Here the same
+launch runs on a 250k x 128 instance of the bench's own data and graph
+recipe: every query's ids and float bits equal the full-visited-set run, a
+sample equals the CPU restatement of searchReadOnlyGraph (Graph.cpp:398-495)
+including the distinct distance count, and the launch keeps full occupancy.
+A second test checks that a 12.5M-row shard (C5's per-GPU size) still gets
+16 resident waves per CU of visited scratch."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from ngt_amd.device import SEED_GIVEN, DeviceIndex
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _cus(torch):
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def test_production_launch_matches_oracle():
+    import torch
+    import bench
+    dev = torch.device("cuda:0")
+    N, D, NQ, K, EPS = 250_000, 128, 8192, 10, 0.05
+    rows = torch.zeros((N + 1, D), dtype=torch.float32, device=dev)
+    rows[1:] = torch.from_numpy(bench.splitmix_uniform(N, D, bench.BASE_SEED)).to(dev)
+    qry = torch.from_numpy(bench.splitmix_uniform(NQ, D, bench.BASE_SEED + 1)).to(dev)
+    offsets, edges = bench.build_graph(torch, rows[1:], 64, 24, 48, 80, dev)
+    ix = DeviceIndex("l2", "float", D)
+    ix.set_objects_device(rows.data_ptr(), N + 1)
+    ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
+    seeds = bench.random_seeds(N + 1, NQ, 10)
+    d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+    d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * 10
+    out = {}
+    for vis in (-2, -1):
+        oi = torch.zeros((NQ, K), dtype=torch.int32, device=dev)
+        od = torch.zeros((NQ, K), dtype=torch.float32, device=dev)
+        on = torch.zeros((NQ,), dtype=torch.int32, device=dev)
+        cnt = torch.zeros((NQ, 8), dtype=torch.int64, device=dev)
+        ix.search_device(qry.data_ptr(), D * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(), cnt.data_ptr(),
+                         k=K, epsilon=EPS, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                         d_seed_off=d_soff.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream,
+                         visited_hash_log2=vis)
+        torch.cuda.synchronize()
+        if vis == -2:
+            assert ix.last_search_slots() == 16 * _cus(torch)
+        out[vis] = (oi.cpu().numpy().view(np.uint32), od.cpu().numpy(), on.cpu().numpy(), cnt.cpu().numpy())
+    a, b = out[-2], out[-1]
+    assert np.array_equal(a[2], b[2])
+    assert np.array_equal(a[0], b[0])
+    assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
+    assert np.all(a[3][:, 0] >= b[3][:, 0])  # re-evaluations of rejected neighbours only add
+    h_rows = rows.cpu().numpy()
+    h_off = offsets.cpu().numpy().astype(np.uint64)  # [N + 2]: node v -> offsets[v]..offsets[v+1]
+    h_edges = edges.cpu().numpy().astype(np.uint32)
+    h_q = qry.cpu().numpy()
+    for i in range(0, NQ, NQ // 48):
+        oid, od, ocnt = O.search("l2", h_rows, h_off, h_edges, h_q[i], seeds[i], K, np.float32(EPS),
+                                 edge_size=0)
+        n = int(a[2][i])
+        assert list(a[0][i, :n]) == list(oid), i
+        assert np.array_equal(a[1][i, :n].view(np.uint32), od.view(np.uint32)), i
+        assert int(b[3][i, 0]) == int(ocnt[0]), i  # the distinct count U(q) the roofline uses
+    ix.close()
+
+
+def test_visited_scratch_full_occupancy_at_shard_size():
+    """A 12.5M-row shard (C5: 100M / 8) keeps 16 resident waves per CU: the
+    visited epochs take slots x rows bytes (51 GB here) from HBM rather than
+    a fixed cap that would cut the slots to ~1.4k."""
+    import torch
+    dev = torch.device("cuda:0")
+    N, D, NQ = 12_500_000, 128, 8192
+    rows = torch.rand((N + 1, D), dtype=torch.float32, device=dev)
+    offs = torch.zeros((N + 2,), dtype=torch.int64, device=dev)
+    edges = torch.zeros((1,), dtype=torch.int32, device=dev)
+    ix = DeviceIndex("l2", "float", D)
+    ix.set_objects_device(rows.data_ptr(), N + 1)
+    ix.set_graph_device(offs.data_ptr(), edges.data_ptr(), 0)
+    rng = np.random.default_rng(5)
+    seeds = rng.integers(1, N + 1, NQ).astype(np.int32)
+    d_seeds = torch.from_numpy(seeds).to(dev)
+    d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev)
+    qry = torch.rand((NQ, D), dtype=torch.float32, device=dev)
+    oi = torch.zeros((NQ, 10), dtype=torch.int32, device=dev)
+    od = torch.zeros((NQ, 10), dtype=torch.float32, device=dev)
+    on = torch.zeros((NQ,), dtype=torch.int32, device=dev)
+    ix.search_device(qry.data_ptr(), D * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None, k=10,
+                     epsilon=0.1, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                     d_seed_off=d_soff.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream,
+                     visited_hash_log2=-2)
+    torch.cuda.synchronize()
+    assert ix.last_search_slots() == 16 * _cus(torch)
+    # a graph without edges returns exactly the seed
+    assert np.all(on.cpu().numpy() == 1)
+    assert np.array_equal(oi[:, 0].cpu().numpy(), seeds)
+    ix.close()
+    del rows
+    torch.cuda.empty_cache()
