@@ -16,10 +16,16 @@ Modes (`--mode`; the default is the headline):
   qg     the NGTQG quantized graph (QuantizedGraph.h:192-320) on the same
          graph: 4-bit codes, dsub = 1 (M = 128 subspaces x 16 centroids),
          exact rerank of k * result_expansion (C5's per-GPU search shape).
+  capi   the drop-in C API on the C2 index: single-query ngt_search_index
+         latency (sequential calls) and the throughput of --threads
+         concurrent single-query callers (coalesced into batched launches,
+         ngt_amd/csrc/coalesce.h); its own JSON line, not the headline.
   shard  C4's form: the object repository sharded one shard per rank (--n
          objects per rank, global ids offset by rank), every rank searches
-         every query on its shard, RCCL all-gather of the per-shard top-k and
-         a device merge (ngt_amd/shard.py); QPS of the whole sharded index.
+         every query on its shard, one RCCL all-gather of the packed per-shard
+         top-k and a device merge (ngt_amd/shard.py); QPS of the whole
+         sharded index.  With --qg, C5's form: every shard is an NGTQG
+         quantized graph (per-shard quantizer, encoder, quantized graph).
 
 Untimed setup: deterministic splitmix64 data (base seed 0x4E4754, queries
 base+1), graph construction (exact kNN by torch GEMM + top-k, then the
@@ -191,7 +197,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mode", choices=["exact", "qg", "shard"], default="exact")
+    ap.add_argument("--mode", choices=["exact", "qg", "shard", "capi"], default="exact")
+    ap.add_argument("--threads", type=int, default=32, help="--mode capi: concurrent C-API callers")
+    ap.add_argument("--qg", action="store_true", help="with --mode shard: NGTQG shards (C5's form)")
     ap.add_argument("--config", choices=["c2", "c3"], default="c2")
     ap.add_argument("--n", type=int, default=0, help="objects (per shard in --mode shard)")
     ap.add_argument("--dim", type=int, default=0)
@@ -217,7 +225,8 @@ def main():
     # (RCCL's init banner, library chatter) goes to stderr
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    if args.mode == "qg" and args.visited == -2:
+    qgm = args.mode == "qg" or (args.mode == "shard" and args.qg)
+    if qgm and args.visited == -2:
         args.visited = -1  # the QG search marks accepted ids only by definition (QuantizedGraph.h:241-266)
     c3 = args.config == "c3"
     if not args.n:
@@ -240,6 +249,8 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from ngt_amd.device import COUNTERS, SEED_GIVEN, DeviceIndex
+    if args.mode == "capi":
+        return capi_bench(args, torch, dev, result_out)
 
     N, D, NQ, K = args.n, args.dim, args.nq, args.k
     dp = ((D - 1) // 16 + 1) * 16
@@ -301,7 +312,7 @@ def main():
     out_i, out_d, out_n, cnt = bufs[0]
     result = {"ids": out_i}
 
-    if args.mode == "qg":
+    if qgm:
         # ngtqg quantize on the device: codebooks (dsub = 1, 16 centroids,
         # 1600-object sample as the reference's dynamic k-means), encoder,
         # quantized graph (QuantizedGraph.h:456-475)
@@ -316,11 +327,13 @@ def main():
     def run(eps, si=0, visited=None):
         oi, od, on, oc = bufs[si]
         visited = args.visited if visited is None else visited
-        if args.mode == "qg":
+        if qgm:
             ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
                                 oc.data_ptr(), k=K, epsilon=eps, result_expansion=args.expansion,
                                 seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
                                 stream=streams[si], visited_hash_log2=visited)
+            if shard:
+                result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
             return
         ix.search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
                          oc.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
@@ -379,7 +392,7 @@ def main():
 
     c = cnt.cpu().numpy().astype(np.float64)
     evals_per_query = None
-    if args.mode != "qg" and args.visited == -2:
+    if not qgm and args.visited == -2:
         # The timed runs keep only accepted ids in the visited set, so their
         # counters include re-evaluations of rejected neighbours.  One more
         # run with every evaluated id in the set gives the reference's distinct
@@ -398,7 +411,7 @@ def main():
         c = cnt.cpu().numpy().astype(np.float64)
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     graph = "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg)
-    if args.mode == "qg":
+    if qgm:
         # B(q) = sum_exp ceil(deg/16)*16*(M/2) + deg*4 + (seeds + k*expansion)*Dp*4  
         me = (D + 1) // 2 * 2
         alg_bytes = c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4 + NQ * (dp * 4 + K * 8)
@@ -439,10 +452,15 @@ def main():
             metric_name = "QPS at recall@10=0.95, %d x %d-d NGTQG quantized graph (L2); achieved HBM GB/s" % (N, D)
             workload = "C5 shape per GPU: %d x %d NGTQG (dsub=1, M=%d, 16 centroids), result_expansion %g, " \
                        "%d queries/step/GPU, k=%d" % (N, D, D, args.expansion, NQ, K)
+        elif qgm:
+            metric_name = "QPS at recall@10=0.95, %d x %d-d NGTQG sharded over %d GPUs" % (N * world, D, world)
+            workload = "C5 form: %d objects per GPU shard (NGTQG dsub=1, M=%d, result_expansion %g), %d shards, " \
+                       "%d queries/step over all shards, k=%d, one packed RCCL all-gather of per-shard top-k + " \
+                       "device merge" % (N, D, args.expansion, world, NQ, K)
         else:
             metric_name = "QPS at recall@10=0.95, %d x %d-d float L2 sharded over %d GPUs" % (N * world, D, world)
             workload = "C4 form: %d objects per GPU shard, %d shards, %d queries/step over all shards, k=%d, " \
-                       "RCCL all-gather of per-shard top-k + device merge" % (N, world, NQ, K)
+                       "one packed RCCL all-gather of per-shard top-k + device merge" % (N, world, NQ, K)
         line = {
             "metric": metric_name,
             "value": qps,
@@ -454,7 +472,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.mode != "qg" else "u4-adc/u8-lut/f32-rerank",
+            "dtype": "f32" if not qgm else "u4-adc/u8-lut/f32-rerank",
             "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
             "config": {"workload": workload,
                        "recall_at_10": rec, "epsilon": chosen, "edge_size": "all", "graph": graph,
@@ -472,7 +490,7 @@ def main():
             "parity_sample": parity,
             "sweep": sweep,
         }
-        if args.mode == "qg":
+        if qgm:
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
             line["config"]["accepted_per_query"] = float(c[:, 1].mean())
@@ -503,6 +521,134 @@ def measured_traffic(mode, config, graph, eps, visited):
                 and e.get("visited", -1) == visited and abs(e["epsilon"] - eps) < 1e-7):
             return float(e["traffic_bytes"])
     return None
+
+
+def write_ngt_index(path, rows, offsets, edges, dim):
+    """The C2 index in the reference's on-disk format (graph-only index, so
+    searches take getRandomSeeds): prf (PropertySet, Common.h:573-666), obj
+    (Repository<Object>: n, then '+' and dim floats per slot, Common.h:1776-1837,
+    ObjectSpace.h:297-312), grp (n, then '+', uint32 count and {uint32 id, float
+    distance} per edge, then the prevsize vector, Graph.h:151-158).  Edge
+    distances are written as 0 (the search never reads them)."""
+    os.makedirs(path, exist_ok=True)
+    n = rows.shape[0]
+    with open(os.path.join(path, "prf"), "w") as f:
+        for k, v in [("Dimension", dim), ("DistanceType", "L2"), ("EdgeSizeForCreation", 10),
+                     ("EdgeSizeForSearch", 0), ("GraphType", "ANNG"), ("IndexType", "Graph"),
+                     ("ObjectType", "Float-4"), ("SeedSize", 10), ("SeedType", "None")]:
+            f.write("%s\t%s\n" % (k, v))
+    rec = np.zeros((n, 1 + 4 * dim), np.uint8)
+    rec[:, 0] = ord("+")
+    rec[:, 1:] = np.ascontiguousarray(rows[:, :dim]).view(np.uint8).reshape(n, 4 * dim)
+    rec[0, 0] = ord("-")
+    with open(os.path.join(path, "obj"), "wb") as f:
+        f.write(np.uint64(n).tobytes())
+        f.write(rec[:1, :1].tobytes())
+        f.write(rec[1:].tobytes())
+    deg = np.diff(offsets.astype(np.int64))
+    with open(os.path.join(path, "grp"), "wb") as f:
+        f.write(np.uint64(n).tobytes())
+        f.write(b"-")
+        pair = np.zeros((len(edges), 2), np.uint32)
+        pair[:, 0] = edges
+        for v in range(1, n):
+            a, b = int(offsets[v]), int(offsets[v + 1])
+            f.write(b"+")
+            f.write(np.uint32(b - a).tobytes())
+            f.write(pair[a:b].tobytes())
+        f.write(np.uint32(0).tobytes())
+    return deg
+
+
+def capi_bench(args, torch, dev, result_out):
+    """Single-query latency and concurrent-caller throughput of the drop-in
+    ngt_search_index (Capi.cpp:346-375) on the C2 data and graph."""
+    import tempfile
+    import threading
+    from ngt_amd import base
+    N, D, NQ, K = args.n, args.dim, args.nq, args.k
+    t0 = time.time()
+    X = splitmix_uniform(N, D, BASE_SEED)
+    Q = splitmix_uniform(NQ, D, BASE_SEED + 1)
+    rows = torch.zeros((N + 1, D), dtype=torch.float32, device=dev)
+    rows[1:] = torch.from_numpy(X).to(dev)
+    offsets, edges = build_graph(torch, rows[1:], args.knn, args.out_deg, args.in_deg, args.max_deg, dev)
+    h_rows, h_off, h_edges = rows.cpu().numpy(), offsets.cpu().numpy(), edges.cpu().numpy().astype(np.uint32)
+    del rows, offsets, edges
+    torch.cuda.empty_cache()
+    tmp = tempfile.mkdtemp(prefix="ngt_c2_")
+    write_ngt_index(tmp, h_rows, h_off, h_edges, D)
+    log("C2 index written in the reference format (%.1f s)" % (time.time() - t0))
+    t0 = time.time()
+    ix = base.Index(tmp)
+    gi, _, _ = ix.batch_linear_search(Q, K)
+    gt = gi.astype(np.int64)
+    log("opened + ground truth (batched C API linear search) in %.1f s" % (time.time() - t0))
+
+    def recall(eps, nq=2000):
+        bi, bd, bn = ix.batch_search(Q[:nq], K, eps, -1.0, -1, graph_only=True)
+        return recall_at(bi.astype(np.int64), gt[:nq], K)
+
+    eps = tune_epsilon(recall, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None)
+    rec = recall(eps, NQ)
+    log("epsilon %.4f recall@10 %.4f (batched C API, graph-only random seeds)" % (eps, rec))
+    # batched C API
+    t0 = time.perf_counter()
+    ix.batch_search(Q, K, eps, -1.0, -1, graph_only=True)
+    batched_qps = NQ / (time.perf_counter() - t0)
+    # single-query latency: sequential ngt_search_index calls
+    lat = []
+    for i in range(min(200, NQ)):
+        t1 = time.perf_counter()
+        ix.search(Q[i].astype(np.float64), K, eps)
+        lat.append(time.perf_counter() - t1)
+    lat = np.array(lat) * 1e3
+    # concurrent single-query callers
+    L = ix._L
+    b0, s0 = ctypes.c_uint64(), ctypes.c_uint64()
+    L.ngt_get_coalesce_stats(ix.index, ctypes.byref(b0), ctypes.byref(s0), ix.err)
+    per = max(1, min(NQ // args.threads, 200))
+    barrier = threading.Barrier(args.threads + 1)
+    hits = [0] * args.threads
+
+    def worker(t):
+        barrier.wait()
+        h = 0
+        for j in range(per):
+            i = t * per + j
+            r = ix.search(Q[i].astype(np.float64), K, eps)
+            h += len(set(x.id for x in r) & set(gt[i].tolist()))
+        hits[t] = h
+        barrier.wait()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(args.threads)]
+    for t in th:
+        t.start()
+    barrier.wait()
+    t1 = time.perf_counter()
+    barrier.wait()
+    el = time.perf_counter() - t1
+    for t in th:
+        t.join()
+    b1, s1 = ctypes.c_uint64(), ctypes.c_uint64()
+    L.ngt_get_coalesce_stats(ix.index, ctypes.byref(b1), ctypes.byref(s1), ix.err)
+    nconc = args.threads * per
+    line = {"metric": "C-API ngt_search_index on C2 (1M x 128 L2): single-query latency and %d-thread throughput"
+                      % args.threads,
+            "value": nconc / el, "unit": "queries/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "f32", "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
+            "config": {"workload": "C2 graph written as an NGT index directory, opened with ngt_open_index",
+                       "epsilon": eps, "recall_at_10_batched": rec,
+                       "recall_at_10_concurrent": sum(hits) / float(nconc * K),
+                       "seeds": "getRandomSeeds (graph-only index)", "threads": args.threads,
+                       "queries_per_thread": per,
+                       "coalesced_launches": int(b1.value - b0.value),
+                       "mean_coalesced_batch": (s1.value - s0.value) / max(1, b1.value - b0.value)},
+            "single_query_latency_ms": {"mean": float(lat.mean()), "p50": float(np.percentile(lat, 50)),
+                                        "p99": float(np.percentile(lat, 99)), "calls": len(lat)},
+            "batched_capi_qps": batched_qps}
+    print(json.dumps(line), file=result_out, flush=True)
+    ix.close()
 
 
 def host_cpu():

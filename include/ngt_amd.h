@@ -232,6 +232,18 @@ int ngt_amd_merge_results_device(int device, const uint32_t *d_ids, const float 
                                  const uint32_t *d_n, uint32_t nparts, uint32_t nq, uint32_t k,
                                  const uint32_t *id_offsets, uint32_t *d_out_ids, float *d_out_dists,
                                  uint32_t *d_out_n, void *stream);
+/* The exchange as ONE message per rank: each result slot packed into a
+ * uint64 {float distance bits << 32 | shard-local id} (the ObjectDistance
+ * pair, 8 B), 0 = empty slot (slot j >= n[q], or the {0, 0} padding of an
+ * NGTQG rerank).  d_packed: [nq][k].  The merge takes the all-gathered
+ * [nparts][nq][k] words and ranks by (distance, global id) like
+ * ngt_amd_merge_results_device. */
+int ngt_amd_pack_results_device(int device, const uint32_t *d_ids, const float *d_dists,
+                                const uint32_t *d_n, uint32_t nq, uint32_t k, uint64_t *d_packed,
+                                void *stream);
+int ngt_amd_merge_packed_device(int device, const uint64_t *d_packed, uint32_t nparts, uint32_t nq,
+                                uint32_t k, const uint32_t *id_offsets, uint32_t *d_out_ids,
+                                float *d_out_dists, uint32_t *d_out_n, void *stream);
 
 /* ---- NGTQG quantized graph (L2, float objects) -------------------------- *
  *   ngt_amd_qg_set_quantizer  <- the NGTQ::Quantizer NGTQG::Index opens from

@@ -80,6 +80,8 @@ def declare(L):
                                            c_uint32]),
         "ngt_amd_merge_results_device": (c_int, [c_int, vp, vp, vp, c_uint32, c_uint32, c_uint32, vp, vp, vp, vp,
                                                  vp]),
+        "ngt_amd_pack_results_device": (c_int, [c_int, vp, vp, vp, c_uint32, c_uint32, vp, vp]),
+        "ngt_amd_merge_packed_device": (c_int, [c_int, vp, c_uint32, c_uint32, c_uint32, vp, vp, vp, vp, vp]),
         "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),
         "ngt_amd_qg_build_graph": (c_int, [vp, vp, c_uint32]),
         "ngt_amd_qg_encode": (c_int, [vp, vp]),

@@ -634,6 +634,9 @@ hipError_t launch_gather_rows(uint8_t* dst, const uint8_t* rows, uint64_t row_by
         case kNormalizedAngle: LAUNCH(kNormalizedAngle, float); break;         \
         case kNormalizedCosine: LAUNCH(kNormalizedCosine, float); break;       \
         case kNormalizedL2: LAUNCH(kNormalizedL2, float); break;               \
+        case kSparseJaccard: LAUNCH(kSparseJaccard, float); break;             \
+        case kPoincare: LAUNCH(kPoincare, float); break;                       \
+        case kLorentz: LAUNCH(kLorentz, float); break;                         \
         default: return hipErrorInvalidValue;                                  \
       }                                                                        \
     } else if ((OTYPE) == kUint8) {                                            \
@@ -644,6 +647,9 @@ hipError_t launch_gather_rows(uint8_t* dst, const uint8_t* rows, uint64_t row_by
         case kJaccard: LAUNCH(kJaccard, uint8_t); break;                       \
         case kAngle: LAUNCH(kAngle, uint8_t); break;                           \
         case kCosine: LAUNCH(kCosine, uint8_t); break;                         \
+        case kNormalizedAngle: LAUNCH(kNormalizedAngle, uint8_t); break;       \
+        case kNormalizedCosine: LAUNCH(kNormalizedCosine, uint8_t); break;     \
+        case kNormalizedL2: LAUNCH(kNormalizedL2, uint8_t); break;             \
         default: return hipErrorInvalidValue;                                  \
       }                                                                        \
     } else {                                                                   \

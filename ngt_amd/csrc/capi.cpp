@@ -122,6 +122,10 @@ std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t 
   p.edge_size = edge_size;
   p.seed_mode = seed_mode;
   p.all_leaf_nodes = 0;
+  // large indexes: visited epochs in HBM from the start (behind the LDS
+  // filter) instead of an LDS hash that would spill after a few thousand ids;
+  // identical results and distance counts either way
+  p.visited_hash_log2 = ix->host.nrows >= (1u << 18) ? -1 : 0;
   ids.resize((size_t)nq * size);
   dists.resize((size_t)nq * size);
   n.resize(nq);

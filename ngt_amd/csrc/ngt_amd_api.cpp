@@ -731,3 +731,39 @@ extern "C" int ngt_amd_merge_results_device(int device, const uint32_t* d_ids, c
   HIP_OK(hipStreamSynchronize(s));
   return 0;
 }
+
+extern "C" int ngt_amd_pack_results_device(int device, const uint32_t* d_ids, const float* d_dists,
+                                           const uint32_t* d_n, uint32_t nq, uint32_t k, uint64_t* d_packed,
+                                           void* stream) {
+  if ((!d_ids || !d_dists || !d_n || !d_packed) && nq) return fail("ngt_amd_pack_results_device: bad arguments");
+  if (nq == 0 || k == 0) return 0;
+  HIP_OK(hipSetDevice(device));
+  HIP_OK(launch_pack_results(d_ids, d_dists, d_n, nq, k, d_packed, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int ngt_amd_merge_packed_device(int device, const uint64_t* d_packed, uint32_t nparts, uint32_t nq,
+                                           uint32_t k, const uint32_t* id_offsets, uint32_t* d_out_ids,
+                                           float* d_out_dists, uint32_t* d_out_n, void* stream) {
+  if (!d_packed || !id_offsets || !d_out_ids || !d_out_dists || !d_out_n || nparts == 0 || k == 0)
+    return fail("ngt_amd_merge_packed_device: bad arguments");
+  if ((uint64_t)nparts * k * sizeof(uint64_t) > 64 * 1024)
+    return fail("ngt_amd_merge_packed_device: %u parts x k=%u exceed one workgroup's LDS", nparts, k);
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = (hipStream_t)stream;
+  DevBuf<uint32_t> off;
+  HIP_OK(off.alloc(nparts));
+  HIP_OK(hipMemcpyAsync(off.p, id_offsets, nparts * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  MergeArgs a{};
+  a.id_offsets = off.p;
+  a.nparts = nparts;
+  a.nq = nq;
+  a.k = k;
+  a.out_ids = d_out_ids;
+  a.out_dists = d_out_dists;
+  a.out_n = d_out_n;
+  HIP_OK(launch_merge_packed(a, d_packed, s));
+  HIP_OK(hipStreamSynchronize(s));  // `off` is freed on return
+  return 0;
+}

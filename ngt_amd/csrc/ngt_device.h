@@ -303,7 +303,10 @@ __device__ __forceinline__ float dist_f32(const float* __restrict__ q,
       }
       while (ai[loca] != 0) loca++;
       while (locb < size && bi[locb] != 0) locb++;
-      r = (float)(1.0 - (double)count / (double)(loca + locb - count));
+      const size_t den = loca + locb - count;
+      // two empty lists: 1 - 0/0 is x86's default NaN, sign bit set (the
+      // reference's bits; a GPU 0/0 would give the positive quiet NaN)
+      r = den == 0 ? __uint_as_float(0xFFC00000u) : (float)(1.0 - (double)count / (double)den);
     }
     return __shfl(r, (lane_id() & ~3), 64);
   } else {

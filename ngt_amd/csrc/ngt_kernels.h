@@ -183,6 +183,9 @@ hipError_t launch_gather_rows(uint8_t* dst, const uint8_t* rows, uint64_t row_by
 
 hipError_t launch_distances(const DistanceArgs& a, int metric, int otype, hipStream_t s);
 hipError_t launch_merge_results(const MergeArgs& a, hipStream_t s);
+hipError_t launch_pack_results(const uint32_t* ids, const float* dists, const uint32_t* n, uint32_t nq, uint32_t k,
+                               uint64_t* out, hipStream_t s);
+hipError_t launch_merge_packed(const MergeArgs& a, const uint64_t* packed, hipStream_t s);
 hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipStream_t s);
 size_t search_lds_bytes(const SearchArgs& a, int otype);
 hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,

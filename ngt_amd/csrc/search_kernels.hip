@@ -520,6 +520,53 @@ __global__ void __launch_bounds__(64) ngt_merge_results_kernel(MergeArgs a) {
   }
 }
 
+// Packed shard messages: one uint64 per result slot, the NGT::ObjectDistance
+// pair {uint32 id, float distance} (Common.h:1937-1992) as (distance bits << 32
+// | shard-local id); 0 = empty (ids are 1-based, ObjectRepository.h:37-40).
+// One all-gather of these [nq][k] words is the whole shard exchange.
+__global__ void __launch_bounds__(256) ngt_pack_results_kernel(const uint32_t* ids, const float* dists,
+                                                               const uint32_t* n, uint32_t nq, uint32_t k,
+                                                               uint64_t* out) {
+  const uint64_t total = (uint64_t)nq * k;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t q = (uint32_t)(i / k), j = (uint32_t)(i - (uint64_t)q * k);
+    const uint32_t id = j < n[q] ? ids[i] : 0u;
+    out[i] = id ? ((uint64_t)__float_as_uint(dists[i]) << 32) | id : 0ull;
+  }
+}
+
+__global__ void __launch_bounds__(64) ngt_merge_packed_kernel(MergeArgs a, const uint64_t* packed) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
+  const int lane = lane_id();
+  const uint32_t total = a.nparts * a.k;
+  for (uint32_t qi = blockIdx.x; qi < a.nq; qi += gridDim.x) {
+    for (uint32_t i = lane; i < total; i += 64) {
+      const uint32_t s = i / a.k, j = i - s * a.k;
+      const uint64_t w = packed[((uint64_t)s * a.nq + qi) * a.k + j];
+      const uint32_t id = (uint32_t)w;
+      keys[i] = id ? make_key(__uint_as_float((uint32_t)(w >> 32)), id + a.id_offsets[s]) : ~0ull;
+    }
+    __syncthreads();
+    uint32_t valid = 0;
+    for (uint32_t i = lane; i < total; i += 64) {
+      const uint64_t key = keys[i];
+      if (key == ~0ull) continue;
+      valid++;
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < total; j++) rank += keys[j] < key ? 1u : 0u;
+      if (rank < a.k) {
+        a.out_ids[(uint64_t)qi * a.k + rank] = key_id(key);
+        a.out_dists[(uint64_t)qi * a.k + rank] = key_dist(key);
+      }
+    }
+    valid = wave_sum_u32(valid);
+    if (lane == 0) a.out_n[qi] = valid < a.k ? valid : a.k;
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launchers (dispatch on metric x object type).
 // ---------------------------------------------------------------------------
@@ -644,6 +691,24 @@ hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint
   if (e != hipSuccess) return e;
   const size_t lds2 = ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   hipLaunchKernelGGL(ngt_linear_merge_kernel, dim3(a.nq), dim3(64), lds2, s, a, nslices);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_results(const uint32_t* ids, const float* dists, const uint32_t* n, uint32_t nq, uint32_t k,
+                               uint64_t* out, hipStream_t s) {
+  const uint64_t total = (uint64_t)nq * k;
+  if (total == 0) return hipSuccess;
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(ngt_pack_results_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, ids, dists, n, nq, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_packed(const MergeArgs& a, const uint64_t* packed, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  const size_t lds = (size_t)a.nparts * a.k * sizeof(uint64_t);
+  const uint32_t blocks = a.nq < 16384 ? a.nq : 16384;
+  hipLaunchKernelGGL(ngt_merge_packed_kernel, dim3(blocks), dim3(64), lds, s, a, packed);
   return hipGetLastError();
 }
 

@@ -1,16 +1,23 @@
-"""Object repository sharded across GPUs (BASELINE config C4).
+"""Object repository sharded across GPUs (BASELINE configs C4
+and C5).
 
 One process per GPU.  Rank r holds shard r -- objects with global ids
-``offset_r + 1 .. offset_r + n_r`` as its own index (rows, graph) in HBM --
-and every rank searches every query on its shard.  The one exchange step is
-an all-gather of the per-shard result lists (``k`` x {uint32 id, float
-distance} per query, RCCL over xGMI when the process group is ``nccl``),
-after which every rank merges the lists on its device with
-``ngt_amd_merge_results_device`` (ObjectDistance ordering: distance, then
-global id -- the result one index over the union would rank).
+``offset_r + 1 .. offset_r + n_r`` as its own index (rows, graph, and for
+NGTQG its quantized graph) in HBM -- and every rank searches every query on
+its shard: the exact best-first search (NeighborhoodGraph::searchReadOnlyGraph,
+Graph.cpp:398-495) or the quantized-graph search (NGTQG::Index::search,
+QuantizedGraph.h:354-372).  The one exchange step is ONE all-gather per batch
+of the packed per-shard result lists: ``k`` 8-byte words per query, each the
+``{uint32 id, float distance}`` pair of NGT::ObjectDistance (Common.h:1937-1992)
+packed as ``distance bits << 32 | local id`` by ``ngt_amd_pack_results_device``
+(0 = empty slot) -- RCCL over xGMI when the process group is ``nccl``, Q*k*8 B
+per rank (800 KB at 10k queries, k = 10).  Every rank then merges the gathered
+words on its device with ``ngt_amd_merge_packed_device``: the k best by
+(distance, global id), the result one index over the union would rank.
 
 The exchange is backend-agnostic (torch.distributed collectives on tensors of
-the merge's device); the CPU tests run it over ``gloo``.
+the merge's device); the CPU tests run it over ``gloo`` with numpy stand-ins
+for the two device kernels (``pack=`` / ``merge=``).
 """
 import numpy as np
 
@@ -35,22 +42,46 @@ def gather_offsets(torch, dist, offset, device):
     return [int(x.item()) for x in out]
 
 
-def exchange(torch, dist, ids, dists, n):
-    """All-gather of the local result lists: [nq, k] ids/dists and [nq] counts
-    -> [world, nq, k] and [world, nq] on every rank (one collective per array,
-    Q*k*8 B per rank)."""
+def pack_device(torch, ids, dists, n, k, stream=None):
+    """[nq, k] ids/dists + [nq] counts -> [nq, k] int64 words (ngt_amd_pack_results_device)."""
+    L = lib()
+    nq = int(n.shape[0])
+    out = torch.empty((nq, k), dtype=torch.int64, device=ids.device)
+    rc = L.ngt_amd_pack_results_device(ids.device.index or 0, ids.data_ptr(), dists.data_ptr(), n.data_ptr(), nq, k,
+                                       out.data_ptr(), stream)
+    if rc != 0:
+        raise NativeError(L.ngt_amd_last_error().decode())
+    return out
+
+
+def exchange_packed(torch, dist, packed):
+    """The one collective: all-gather of every rank's [nq, k] packed words ->
+    [world, nq, k] on every rank."""
     world = dist.get_world_size()
-    out = []
-    for t in (ids, dists, n):
-        # rank-major concatenation along dim 0 (the layout every backend accepts)
-        g = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(g, t.contiguous())
-        out.append(g.view((world,) + tuple(t.shape)))
-    return tuple(out)
+    g = torch.empty((world * packed.shape[0],) + tuple(packed.shape[1:]), dtype=packed.dtype, device=packed.device)
+    dist.all_gather_into_tensor(g, packed.contiguous())
+    return g.view((world,) + tuple(packed.shape))
+
+
+def merge_packed_device(torch, g_packed, offsets, k, stream=None):
+    """Device merge of gathered packed words (ngt_amd_merge_packed_device)."""
+    L = lib()
+    world, nq = int(g_packed.shape[0]), int(g_packed.shape[1])
+    dev = g_packed.device
+    out_i = torch.zeros((nq, k), dtype=torch.int32, device=dev)
+    out_d = torch.zeros((nq, k), dtype=torch.float32, device=dev)
+    out_n = torch.zeros((nq,), dtype=torch.int32, device=dev)
+    off = np.ascontiguousarray(offsets, dtype=np.uint32)
+    rc = L.ngt_amd_merge_packed_device(dev.index or 0, g_packed.data_ptr(), world, nq, k, off.ctypes.data,
+                                       out_i.data_ptr(), out_d.data_ptr(), out_n.data_ptr(), stream)
+    if rc != 0:
+        raise NativeError(L.ngt_amd_last_error().decode())
+    return out_i, out_d, out_n
 
 
 def merge_device(torch, g_ids, g_d, g_n, offsets, k, stream=None):
-    """Device merge of gathered shard lists (ngt_amd_merge_results_device)."""
+    """Device merge of gathered unpacked lists (ngt_amd_merge_results_device):
+    [world, nq, k] ids/dists and [world, nq] counts."""
     L = lib()
     world, nq = int(g_n.shape[0]), int(g_n.shape[1])
     dev = g_ids.device
@@ -70,28 +101,57 @@ class ShardedIndex(object):
     """Search front end of one rank's shard.  `index` is the rank's
     DeviceIndex (ids 1..n_r local); `offset` its global id offset."""
 
-    def __init__(self, torch, dist, index, offset, device, merge=merge_device):
+    def __init__(self, torch, dist, index, offset, device, pack=pack_device, merge=merge_packed_device):
         self.torch, self.dist, self.index = torch, dist, index
         self.device = device
         self.offsets = gather_offsets(torch, dist, offset, device)
+        self.pack = pack
         self.merge = merge
 
     def merge_local(self, ids, dists, n, k, stream=None):
-        """Exchange + merge of already computed local results (tensors)."""
-        g_ids, g_d, g_n = exchange(self.torch, self.dist, ids, dists, n)
-        return self.merge(self.torch, g_ids, g_d, g_n, self.offsets, k, stream)
+        """Pack, exchange (one all-gather) and merge already computed local
+        results (tensors [nq, k], [nq, k], [nq])."""
+        t = self.torch
+        packed = self.pack(t, ids, dists, n, k, stream)
+        ext = None
+        if stream is not None and ids.is_cuda:
+            # the collective is ordered after torch's current stream: make that
+            # stream wait for the search + pack on `stream`, and the merge wait
+            # for the collective
+            ext = t.cuda.ExternalStream(stream, device=self.device)
+            t.cuda.current_stream(self.device).wait_stream(ext)
+        g = exchange_packed(t, self.dist, packed)
+        if ext is not None:
+            ext.wait_stream(t.cuda.current_stream(self.device))
+        return self.merge(t, g, self.offsets, k, stream)
+
+    def _out(self, nq, k):
+        t = self.torch
+        return (t.zeros((nq, k), dtype=t.int32, device=self.device), t.zeros((nq, k), dtype=t.float32, device=self.device),
+                t.zeros((nq,), dtype=t.int32, device=self.device))
 
     def search_device(self, d_queries, query_bytes, nq, k, epsilon, seeds=None, seed_off=None, stream=None,
                       visited_hash_log2=0, edge_size=-1, seed_mode=None):
         """Local graph search of nq device queries on this shard, then the
         exchange and merge; returns global (ids, dists, n) tensors."""
         from .device import SEED_GIVEN, SEED_TREE
-        torch = self.torch
-        ids = torch.zeros((nq, k), dtype=torch.int32, device=self.device)
-        ds = torch.zeros((nq, k), dtype=torch.float32, device=self.device)
-        n = torch.zeros((nq,), dtype=torch.int32, device=self.device)
+        ids, ds, n = self._out(nq, k)
         mode = seed_mode if seed_mode is not None else (SEED_GIVEN if seeds is not None else SEED_TREE)
         self.index.search_device(d_queries, query_bytes, nq, ids.data_ptr(), ds.data_ptr(), n.data_ptr(), None,
                                  k=k, epsilon=epsilon, edge_size=edge_size, seed_mode=mode, d_seeds=seeds,
                                  d_seed_off=seed_off, stream=stream, visited_hash_log2=visited_hash_log2)
+        return self.merge_local(ids, ds, n, k, stream)
+
+    def qg_search_device(self, d_queries, query_bytes, nq, k, epsilon, result_expansion=3.0, seeds=None,
+                         seed_off=None, stream=None, visited_hash_log2=-1, seed_mode=None):
+        """C5's form: the NGTQG search (QuantizedGraph.h:354-372) of nq device
+        queries on this shard's quantized graph (exact rerank of k * expansion
+        included), then the same exchange and merge of the reranked top-k."""
+        from .device import SEED_GIVEN, SEED_TREE
+        ids, ds, n = self._out(nq, k)
+        mode = seed_mode if seed_mode is not None else (SEED_GIVEN if seeds is not None else SEED_TREE)
+        self.index.qg_search_device(d_queries, query_bytes, nq, ids.data_ptr(), ds.data_ptr(), n.data_ptr(), None,
+                                    k=k, epsilon=epsilon, result_expansion=result_expansion, seed_mode=mode,
+                                    d_seeds=seeds, d_seed_off=seed_off, stream=stream,
+                                    visited_hash_log2=visited_hash_log2)
         return self.merge_local(ids, ds, n, k, stream)

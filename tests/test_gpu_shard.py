@@ -1,7 +1,9 @@
-"""GPU side of the sharded path: the device merge kernel
-(ngt_amd_merge_results_device) against a numpy merge of the same lists, and
-the full ShardedIndex pipeline (local graph search -> RCCL all-gather ->
-device merge) on a one-rank nccl group, against the oracle."""
+"""GPU side of the sharded path: the device merge kernels
+(ngt_amd_merge_results_device, ngt_amd_pack_results_device +
+ngt_amd_merge_packed_device) against a numpy merge of the same lists, and the
+full ShardedIndex pipeline (local exact or NGTQG search -> one packed RCCL
+all-gather -> device merge) on a one-rank nccl group, against the oracle and
+the reference's own NGTQG results."""
 import os
 import socket
 
@@ -55,6 +57,50 @@ def test_merge_kernel_matches_numpy(S, k):
         assert np.array_equal(gd[q, :gn[q]].view(np.uint32), ed[q, :en[q]].view(np.uint32))
 
 
+@pytest.mark.parametrize("S,k", [(2, 10), (8, 10), (8, 100), (3, 1)])
+def test_pack_and_packed_merge_match_numpy(S, k):
+    """The exchange message (ngt_amd_pack_results_device: distance bits << 32 |
+    local id, 0 = empty) and its merge (ngt_amd_merge_packed_device) against a
+    numpy merge, with ragged lists, empty lists and exact distance ties."""
+    import torch
+    from ngt_amd.shard import merge_packed_device, pack_device
+    rng = np.random.default_rng(S * 31 + k)
+    nq = 257
+    ids = np.zeros((S, nq, k), np.uint32)
+    ds = np.zeros((S, nq, k), np.float32)
+    n = rng.integers(0, k + 1, size=(S, nq)).astype(np.uint32)
+    n[:, 0] = k
+    n[:, 1] = 0
+    offsets = [s * 1000 for s in range(S)]
+    for s in range(S):
+        for q in range(nq):
+            d = np.sort(rng.integers(0, 50, k).astype(np.float32) / np.float32(7))
+            ids[s, q] = rng.choice(np.arange(1, 1000), k, replace=False)
+            order = np.lexsort((ids[s, q], d))
+            ids[s, q], ds[s, q] = ids[s, q][order], d[order]
+    dev = torch.device("cuda:0")
+    packed = []
+    for s in range(S):
+        packed.append(pack_device(torch, torch.from_numpy(ids[s].view(np.int32)).to(dev),
+                                  torch.from_numpy(ds[s]).to(dev), torch.from_numpy(n[s].view(np.int32)).to(dev), k))
+    g = torch.stack(packed)
+    torch.cuda.synchronize()
+    w = g.cpu().numpy().view(np.uint64)
+    for s in range(S):
+        for q in range(0, nq, 17):
+            for j in range(k):
+                exp = (int(ds[s, q, j].view(np.uint32)) << 32 | int(ids[s, q, j])) if j < n[s, q] else 0
+                assert int(w[s, q, j]) == exp, (s, q, j)
+    gi, gd, gn = merge_packed_device(torch, g, offsets, k)
+    torch.cuda.synchronize()
+    ei, ed, en = np_merge(ids, ds, n, offsets, k)
+    gi, gd, gn = gi.cpu().numpy().view(np.uint32), gd.cpu().numpy(), gn.cpu().numpy()
+    assert np.array_equal(gn, en)
+    for q in range(nq):
+        assert list(gi[q, :gn[q]]) == list(ei[q, :en[q]]), q
+        assert np.array_equal(gd[q, :gn[q]].view(np.uint32), ed[q, :en[q]].view(np.uint32))
+
+
 def test_sharded_index_one_rank_nccl():
     import torch
     import torch.distributed as dist
@@ -93,5 +139,31 @@ def test_sharded_index_one_rank_nccl():
             assert list(gi[i, :gn[i]]) == list(oid + off), i
             assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32))
         ix.close()
+
+        # C5's form: the NGTQG search on the shard, then the same exchange and
+        # merge -- on the reference's C1 quantized graph, against the
+        # reference's own NGTQG::Index::search results (tests/golden/c1_qg)
+        from test_gpu_qg import device_qg, state
+        _, _, _, _, _, _, _, z, meta, dim, _ = state("c1_qg")
+        qix = device_qg("c1_qg")
+        qsq = z["queries"].astype(np.float32)
+        d_q = torch.from_numpy(qsq).to(dev)
+        sq = ShardedIndex(torch, dist, qix, 0, dev)
+        from ngt_amd.device import SEED_TREE
+        for key in ("10_0.05_3", "20_0.03_3", "10_0.1_2"):
+            k, eps, exp = key.split("_")
+            gi, gd, gn = sq.qg_search_device(d_q.data_ptr(), dim * 4, len(qsq), int(k), float(eps),
+                                             result_expansion=float(exp), stream=stream, seed_mode=SEED_TREE)
+            torch.cuda.synchronize()
+            gi, gd, gn = gi.cpu().numpy().view(np.uint32), gd.cpu().numpy(), gn.cpu().numpy()
+            for qi in range(len(qsq)):
+                n = int(z["n_" + key][qi])
+                ref_ids = z["ids_" + key][qi][:n]
+                valid = ref_ids != 0  # the reference pads a short rerank with {0, 0}
+                assert int(gn[qi]) == int(valid.sum()), (key, qi)
+                assert list(gi[qi, :gn[qi]]) == list(ref_ids[valid]), (key, qi)
+                assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32),
+                                      z["dist_" + key][qi][:n][valid].view(np.uint32)), (key, qi)
+        qix.close()
     finally:
         dist.destroy_process_group()

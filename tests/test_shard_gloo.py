@@ -28,16 +28,30 @@ def _data():
     return rows, qs
 
 
-def numpy_merge(torch, g_ids, g_d, g_n, offsets, k, stream=None):
-    world, nq = g_n.shape[0], g_n.shape[1]
+def numpy_pack(torch, ids, dists, n, k, stream=None):
+    """Checker of ngt_amd_pack_results_device's contract: distance bits << 32 |
+    local id per valid slot, 0 for empty slots."""
+    i = ids.numpy().view(np.uint32).astype(np.uint64)
+    d = dists.numpy().view(np.uint32).astype(np.uint64)
+    valid = (np.arange(k)[None, :] < n.numpy()[:, None]) & (i != 0)
+    return torch.from_numpy(np.where(valid, (d << np.uint64(32)) | i, np.uint64(0)).view(np.int64))
+
+
+def numpy_merge(torch, g_packed, offsets, k, stream=None):
+    """Checker of ngt_amd_merge_packed_device's contract."""
+    w = g_packed.numpy().view(np.uint64)
+    world, nq = w.shape[0], w.shape[1]
     out_i = torch.zeros((nq, k), dtype=torch.int32)
     out_d = torch.zeros((nq, k), dtype=torch.float32)
     out_n = torch.zeros((nq,), dtype=torch.int32)
     for q in range(nq):
         cand = []
         for s in range(world):
-            for j in range(int(g_n[s, q])):
-                cand.append((float(g_d[s, q, j]), int(g_ids[s, q, j]) + offsets[s]))
+            for j in range(k):
+                x = int(w[s, q, j])
+                if x:
+                    d = np.array([x >> 32], np.uint32).view(np.float32)[0]
+                    cand.append((float(d), (x & 0xFFFFFFFF) + offsets[s]))
         cand.sort()
         for j, (d, i) in enumerate(cand[:k]):
             out_i[q, j] = i
@@ -65,7 +79,7 @@ def _worker(rank, world, port, q):
             n[i] = len(oi)
             ids[i, :n[i]] = oi
             ds[i, :n[i]] = od
-        sx = ShardedIndex(torch, dist, None, off, torch.device("cpu"), merge=numpy_merge)
+        sx = ShardedIndex(torch, dist, None, off, torch.device("cpu"), pack=numpy_pack, merge=numpy_merge)
         gi, gd, gn = sx.merge_local(torch.from_numpy(ids), torch.from_numpy(ds), torch.from_numpy(n), K)
         q.put((rank, off, cnt, sx.offsets, gi.numpy(), gd.numpy(), gn.numpy()))
     finally:
