@@ -144,6 +144,13 @@ bool ngt_optimize_number_of_edges(const char *indexPath, NGTAnngEdgeOptimization
 bool ngt_set_property_distance_type_normalized_l2(NGTProperty, NGTError);
 bool ngt_set_property_distance_type_sparse_jaccard(NGTProperty, NGTError);
 
+/* ---- extensions: any NGT::Property field by its prf key (PropertySet,
+ * Common.h:573-666; keys of Index.h:105-261 and Graph.h:423-489), the way the
+ * C++ facade (include/NGT/Index.h) reads and writes NGT::Property ------- */
+bool ngt_set_property_value(NGTProperty, const char *key, const char *value, NGTError);
+/* value into buf (truncated to len - 1 chars); returns its full length, -1 if absent */
+int32_t ngt_get_property_value(NGTProperty, const char *key, char *buf, size_t len, NGTError);
+
 /* ---- extensions: batched device search ---------------------------------- */
 /* queries: [nq][dim] floats.  ids/dists: [nq][size], n: [nq] (results per query). */
 bool ngt_batch_search_index(NGTIndex, const float *queries, uint32_t nq, int32_t dim, size_t size,
@@ -161,8 +168,10 @@ bool ngt_batch_linear_search_index(NGTIndex, const float *queries, uint32_t nq, 
 bool ngt_batch_linear_search_index_with_radius(NGTIndex, const float *queries, uint32_t nq,
                                                int32_t dim, size_t size, float radius, uint32_t *ids,
                                                float *dists, uint32_t *n, NGTError);
-/* counters of this thread's last search on this handle: [0] distance
- * computations, [1] evaluated neighbours, [2] expansions (summed over its queries) */
+/* counters of this thread's last search on this handle, summed over its
+ * queries, with the reference's read-write SearchContainer semantics
+ * (Graph.cpp:588-604): [0] distanceComputationCount (neighbour distances; the
+ * seeds' are not counted), [1] visitCount (edges scanned), [2] expansions */
 bool ngt_get_last_search_counters(NGTIndex, uint64_t *counters3, NGTError);
 /* single-query calls served so far: device launches issued and queries served
  * by them (served / batches = mean coalesced batch size) */

@@ -48,6 +48,9 @@ typedef struct {
 } NGTQGQuantizationParameters;
 
 NGTQGIndex ngtqg_open_index(const char *, NGTError);
+/* extension: NGTQG::Index(path, maxNoOfEdges) (QuantizedGraph.h:170-185) --
+ * the quantized graph built at open keeps at most max_edges neighbours/node */
+NGTQGIndex ngtqg_open_index_with_max_edges(const char *, uint32_t max_edges, NGTError);
 
 void ngtqg_close_index(NGTQGIndex);
 

@@ -164,8 +164,11 @@ def declare(L):
                                                                u32p, f32p, u32p, vp]),
         "ngt_get_last_search_counters": (c_bool, [vp, u64p, vp]),
         "ngt_get_coalesce_stats": (c_bool, [vp, u64p, u64p, vp]),
+        "ngt_set_property_value": (c_bool, [vp, c_char_p, c_char_p, vp]),
+        "ngt_get_property_value": (c_int32, [vp, c_char_p, c_char_p, c_size_t, vp]),
         # ---- include/NGT/NGTQ/Capi.h
         "ngtqg_open_index": (vp, [c_char_p, vp]),
+        "ngtqg_open_index_with_max_edges": (vp, [c_char_p, c_uint32, vp]),
         "ngtqg_close_index": (None, [vp]),
         "ngtqg_initialize_quantization_parameters": (None, [POINTER(NGTQGQuantizationParameters)]),
         "ngtqg_quantize": (c_bool, [c_char_p, NGTQGQuantizationParameters, vp]),

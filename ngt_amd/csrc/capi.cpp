@@ -133,9 +133,18 @@ std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t 
   if (ngt_amd_search(ix->dev, &p, queries, nq, nullptr, nullptr, ids.data(), dists.data(), n.data(),
                      cnt.data()))
     return amd_err();
+  // the reference's SearchContainer counters of a read-write search
+  // (NeighborhoodGraph::search, Graph.cpp:588-604): distanceComputationCount
+  // counts neighbour distances (seed distances only under
+  // NGT_DISTANCE_COMPUTATION_COUNT, off by default, :287), visitCount every
+  // scanned edge; then expansions
   t_last_counters[0] = t_last_counters[1] = t_last_counters[2] = 0;
-  for (uint32_t q = 0; q < nq; q++)
-    for (int c = 0; c < 3; c++) t_last_counters[c] += cnt[(size_t)q * NGT_AMD_COUNTERS_PER_QUERY + c];
+  for (uint32_t q = 0; q < nq; q++) {
+    const uint64_t* c = cnt.data() + (size_t)q * NGT_AMD_COUNTERS_PER_QUERY;
+    t_last_counters[0] += c[1];
+    t_last_counters[1] += c[4];
+    t_last_counters[2] += c[2];
+  }
   if (per_query) *per_query = std::move(cnt);
   return "";
 }
@@ -551,8 +560,12 @@ static std::string single_query(CapiIndex* ix, int kind, const float* q, size_t 
       b->n = vn[i];
       b->ids.assign(vi.begin() + (size_t)i * k.size, vi.begin() + (size_t)i * k.size + vn[i]);
       b->dists.assign(vd.begin() + (size_t)i * k.size, vd.begin() + (size_t)i * k.size + vn[i]);
-      if (!cnt.empty())
-        for (int c = 0; c < 3; c++) b->counters[c] = cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + c];
+      if (!cnt.empty()) {
+        const uint64_t* c = cnt.data() + (size_t)i * NGT_AMD_COUNTERS_PER_QUERY;
+        b->counters[0] = c[1];
+        b->counters[1] = c[4];
+        b->counters[2] = c[2];
+      }
     }
   });
   if (r.err.empty()) {
@@ -1020,6 +1033,37 @@ bool ngt_get_last_search_counters(NGTIndex index, uint64_t* counters3, NGTError 
   }
   memcpy(counters3, t_last_counters, 3 * sizeof(uint64_t));
   return true;
+}
+
+bool ngt_set_property_value(NGTProperty prop, const char* key, const char* value, NGTError error) {
+  if (prop == NULL || key == NULL || value == NULL) {
+    param_error(error, __FUNCTION__, "null argument");
+    return false;
+  }
+  HostProperty* p = prop_of(prop);
+  p->to_kv();
+  p->kv[key] = value;
+  p->from_kv();
+  return true;
+}
+
+int32_t ngt_get_property_value(NGTProperty prop, const char* key, char* buf, size_t len, NGTError error) {
+  if (prop == NULL || key == NULL) {
+    param_error(error, __FUNCTION__, "null argument");
+    return -1;
+  }
+  HostProperty* p = prop_of(prop);
+  p->to_kv();
+  auto it = p->kv.find(key);
+  if (it == p->kv.end()) {
+    set_error(error, __FUNCTION__, std::string("no property ") + key);
+    return -1;
+  }
+  if (buf && len) {
+    strncpy(buf, it->second.c_str(), len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int32_t)it->second.size();
 }
 
 bool ngt_get_coalesce_stats(NGTIndex index, uint64_t* batches, uint64_t* served, NGTError error) {

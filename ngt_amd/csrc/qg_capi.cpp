@@ -45,7 +45,7 @@ void report(NGTError error, const std::string& msg) {
 
 std::string amd_err() { return std::string(ngt_amd_last_error()); }
 
-std::string open_device(QgCapiIndex* ix) {
+std::string open_device(QgCapiIndex* ix, uint32_t max_edges) {
   using ngt_amd::HostIndex;
   HostIndex& h = ix->host;
   if (h.prop.distance_type != NGT_AMD_DISTANCE_L2 || h.prop.object_type != NGT_AMD_OBJECT_FLOAT)
@@ -71,8 +71,8 @@ std::string open_device(QgCapiIndex* ix) {
     if (ngt_amd_qg_set_graph(ix->dev, q.qoff.data(), q.qids.data(), q.code_off.data(), q.qcodes.data()))
       return amd_err();
   } else {
-    // QuantizedGraphRepository::construct with the default maxNoOfEdges (QuantizedGraph.h:170)
-    if (ngt_amd_qg_build_graph(ix->dev, q.codes.data(), 128)) return amd_err();
+    // QuantizedGraphRepository::construct with maxNoOfEdges (default 128, QuantizedGraph.h:170)
+    if (ngt_amd_qg_build_graph(ix->dev, q.codes.data(), max_edges)) return amd_err();
   }
   return "";
 }
@@ -203,13 +203,18 @@ void ngtqg_initialize_quantization_parameters(NGTQGQuantizationParameters* param
 }
 
 NGTQGIndex ngtqg_open_index(const char* index_path, NGTError error) {
+  return ngtqg_open_index_with_max_edges(index_path, 128, error);
+}
+
+NGTQGIndex ngtqg_open_index_with_max_edges(const char* index_path, uint32_t max_edges, NGTError error) {
   auto* ix = new QgCapiIndex();
   std::string e;
   if (!index_path) e = "null index path";
   if (e.empty()) e = ngt_amd::load_index(index_path, ix->host);
   if (e.empty()) e = ngt_amd::load_qg(index_path, ix->host.nrows, ix->quant);
   if (e.empty() && (int64_t)ix->quant.dim != ix->host.prop.dimension) e = "qg/prf dimension differs from the index";
-  if (e.empty()) e = open_device(ix);
+  if (e.empty() && max_edges == 0) e = "max_edges must be > 0";
+  if (e.empty()) e = open_device(ix, max_edges);
   if (!e.empty()) {
     report(error, std::string("Capi : ") + __FUNCTION__ + "() : Error: " + e);
     delete ix;
