@@ -62,7 +62,7 @@ extern "C" {
 /* Seed providers (NeighborhoodGraph::SeedType, lib/NGT/Graph.h:279-285). */
 #define NGT_AMD_SEED_TREE 0    /* DVP-tree leaf (GraphAndTreeIndex::search)        */
 #define NGT_AMD_SEED_GIVEN 1   /* caller-supplied seed lists (search(sc, seeds))    */
-#define NGT_AMD_SEED_RANDOM 2  /* getRandomSeeds over the process rand() stream     */
+#define NGT_AMD_SEED_RANDOM 2  /* getRandomSeeds over the library's rand() stream   */
 
 typedef struct ngt_amd_index ngt_amd_index;
 
@@ -93,6 +93,11 @@ typedef struct {
 
 const char *ngt_amd_last_error(void);
 int ngt_amd_device_count(void);
+/* Reseed the rand() stream NGT_AMD_SEED_RANDOM searches draw from.  It is a
+ * glibc random(3) TYPE_3 sequence private to the library, seeded 1 at load --
+ * what a fresh reference process's rand() returns (GraphIndex::getRandomSeeds,
+ * lib/NGT/Index.h:775-801) -- so other rand() users cannot shift it. */
+void ngt_amd_srand(unsigned int seed);
 
 /* ---- index ------------------------------------------------------------- */
 int ngt_amd_index_create(ngt_amd_index **out, int device, int distance_type,

@@ -67,6 +67,7 @@ def declare(L):
                                                  vp]),
         "ngt_amd_distances": (c_int, [vp, vp, c_uint32, vp, vp, c_uint64, vp]),
         "ngt_amd_prepare_queries_device": (c_int, [vp, vp, c_uint32, vp, vp]),
+        "ngt_amd_srand": (None, [c_uint]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
         "ngt_amd_last_search_slots": (c_uint32, [vp]),
         "ngt_amd_build_begin": (c_int, [vp, POINTER(BuildParams)]),

@@ -236,7 +236,8 @@ struct CallGuard {
 int run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queries, uint64_t query_bytes, uint32_t nq,
                    uint32_t k, int all_leaf_nodes, hipStream_t s);
 float coef_of(float epsilon);
-// GraphIndex::getRandomSeeds (Index.h:775-801) over the process rand() stream
+// GraphIndex::getRandomSeeds (Index.h:775-801) over the library's rand() stream
+// (a fresh process's glibc sequence, ngt_amd_srand)
 std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off);
 // host float queries [nq][dim] -> prepared device rows (Index::allocateObject)
 int upload_queries(ngt_amd_index* ix, const void* queries, uint32_t nq, DevBuf<float>& raw,

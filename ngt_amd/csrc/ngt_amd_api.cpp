@@ -473,9 +473,33 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   return 0;
 }
 
+// The rand() stream getRandomSeeds draws from.  The reference calls the
+// process-wide glibc rand(), so a fresh `ngt search -i g` process draws from
+// seed 1.  The GPU runtime in this process may call rand() itself, which
+// would shift that stream between searches; the library therefore keeps its
+// own glibc TYPE_3 generator (random_r restated, index_internal.h), seeded 1
+// like a fresh process and reseeded only by ngt_amd_srand -- the reference's
+// sequence, independent of anything else in the process.
+static std::mutex g_rand_mu;
+static GlibcRandHost& seed_rand() {
+  static GlibcRandHost r = [] {
+    GlibcRandHost g;
+    g.seed(1);
+    return g;
+  }();
+  return r;
+}
+
+extern "C" void ngt_amd_srand(unsigned int seed) {
+  std::lock_guard<std::mutex> lk(g_rand_mu);
+  seed_rand().seed(seed);
+}
+
 std::vector<uint32_t> ngt_amd::random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off) {
-  // GraphIndex::getRandomSeeds (Index.h:775-801) over the process-wide rand()
-  // stream, one query after another as the reference's callers do.
+  // GraphIndex::getRandomSeeds (Index.h:775-801) over the rand() stream, one
+  // query after another as the reference's callers do.
+  std::lock_guard<std::mutex> lk(g_rand_mu);
+  GlibcRandHost& rnd = seed_rand();
   std::vector<uint32_t> seeds;
   off.assign(nq + 1, 0);
   size_t repo = ix->nrows == 0 ? 0 : ix->nrows - 1;
@@ -484,7 +508,7 @@ std::vector<uint32_t> ngt_amd::random_seed_lists(ngt_amd_index* ix, uint32_t nq,
     size_t start = seeds.size();
     size_t empty = 0;
     while (seeds.size() - start < ss) {
-      double random = ((double)rand() + 1.0) / ((double)RAND_MAX + 2.0);
+      double random = ((double)rnd.next() + 1.0) / ((double)RAND_MAX + 2.0);
       size_t idx = (size_t)floor((double)repo * random) + 1;
       if (ix->h_graph_empty[idx]) {
         if (++empty > repo) break;
@@ -511,11 +535,7 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
   if (!c) return -1;
   if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
-    std::vector<uint32_t> seeds;
-    {
-      std::lock_guard<std::mutex> lk(ix->mu);  // one query after another on the rand() stream
-      seeds = random_seed_lists(ix, nq, off);
-    }
+    std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
     HIP_OK(c->seed_off.upload(off.data(), off.size()));
     HIP_OK(c->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
     return run_search(ix, c, prm, d_queries, query_bytes, nq, c->seeds.p, c->seed_off.p, d_ids,

@@ -370,11 +370,7 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
     a.seed_count = c->seed_count.p;
   } else if (prm->seed_mode == NGT_AMD_SEED_RANDOM) {
     std::vector<uint64_t> off;
-    std::vector<uint32_t> seeds;
-    {
-      std::lock_guard<std::mutex> lk(ix->mu);  // one query after another on the rand() stream
-      seeds = random_seed_lists(ix, nq, off);
-    }
+    std::vector<uint32_t> seeds = random_seed_lists(ix, nq, off);
     HIP_OK(c->seed_off.upload(off.data(), off.size()));
     HIP_OK(c->seeds.upload(seeds.data(), std::max<size_t>(seeds.size(), 1)));
     a.seeds = c->seeds.p;

@@ -202,11 +202,7 @@ void ngtqg_initialize_quantization_parameters(NGTQGQuantizationParameters* param
   parameters->max_number_of_edges = 128;
 }
 
-NGTQGIndex ngtqg_open_index(const char* index_path, NGTError error) {
-  return ngtqg_open_index_with_max_edges(index_path, 128, error);
-}
-
-NGTQGIndex ngtqg_open_index_with_max_edges(const char* index_path, uint32_t max_edges, NGTError error) {
+static NGTQGIndex open_qg(const char* func, const char* index_path, uint32_t max_edges, NGTError error) {
   auto* ix = new QgCapiIndex();
   std::string e;
   if (!index_path) e = "null index path";
@@ -216,12 +212,20 @@ NGTQGIndex ngtqg_open_index_with_max_edges(const char* index_path, uint32_t max_
   if (e.empty() && max_edges == 0) e = "max_edges must be > 0";
   if (e.empty()) e = open_device(ix, max_edges);
   if (!e.empty()) {
-    report(error, std::string("Capi : ") + __FUNCTION__ + "() : Error: " + e);
+    report(error, std::string("Capi : ") + func + "() : Error: " + e);
     delete ix;
     return NULL;
   }
   ix->co.reset(new ngt_amd::Coalescer((uint32_t)ix->host.prop.dimension));
   return static_cast<NGTQGIndex>(ix);
+}
+
+NGTQGIndex ngtqg_open_index(const char* index_path, NGTError error) {
+  return open_qg(__FUNCTION__, index_path, 128, error);
+}
+
+NGTQGIndex ngtqg_open_index_with_max_edges(const char* index_path, uint32_t max_edges, NGTError error) {
+  return open_qg(__FUNCTION__, index_path, max_edges, error);
 }
 
 void ngtqg_close_index(NGTQGIndex index) {

@@ -122,14 +122,19 @@ def test_k20_search_matches_reference(name):
 @pytest.mark.parametrize("name", ["c1_anng", "c1_onng"])
 @pytest.mark.parametrize("eps", ["0.0", "0.1"])
 def test_graph_only_search_matches_reference(name, eps):
-    """`ngt search -i g`: random seeds from the process rand() stream (seed 1)."""
+    """`ngt search -i g`: random seeds from a fresh process's rand() stream
+    (seed 1), one query after another -- in one batch and query by query."""
+    from ngt_amd import lib
     ix, *_ = device_index(name)
-    libc = ctypes.CDLL("libc.so.6")
-    libc.srand(1)
+    lib().ngt_amd_srand(1)
     gi, gd, gn, _ = ix.search(queries(), k=10, epsilon=float(eps), seed_mode=SEED_RANDOM)
     g = np.load(os.path.join(GOLD, "search_%s_gr_%s.npz" % (name, eps)))
     for i in range(len(queries())):
         assert list(gi[i, :gn[i]]) == list(g["ids"][i][g["ids"][i] >= 0]), i
+    lib().ngt_amd_srand(1)
+    for i in range(len(queries())):
+        si, sd, sn, _ = ix.search(queries()[i:i + 1], k=10, epsilon=float(eps), seed_mode=SEED_RANDOM)
+        assert list(si[0, :sn[0]]) == list(g["ids"][i][g["ids"][i] >= 0]), i
     ix.close()
 
 
