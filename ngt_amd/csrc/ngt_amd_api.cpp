@@ -528,6 +528,9 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
                                      uint32_t* d_ids, float* d_dists, uint32_t* d_n,
                                      uint64_t* d_counters, void* stream) {
   if (!ix || !prm || (!d_queries && nq)) return fail("ngt_amd_search_device: bad arguments");
+  if (nq && query_bytes < ix->row_bytes)
+    return fail("ngt_amd_search_device: query stride %llu < %llu bytes (queries are prepared rows of the padded dimension)",
+                (unsigned long long)query_bytes, (unsigned long long)ix->row_bytes);
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
   hipStream_t s = (hipStream_t)stream;  // null = the default stream
@@ -632,17 +635,14 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
                                             uint32_t nq, uint32_t k, double radius, uint32_t* d_ids,
                                             float* d_dists, uint32_t* d_n, void* stream) {
   if (!ix || (!d_queries && nq) || k == 0) return fail("ngt_amd_linear_search_device: bad arguments");
+  if (nq && query_bytes < ix->row_bytes)
+    return fail("ngt_amd_linear_search_device: query stride %llu < %llu bytes (queries are prepared rows of the padded dimension)",
+                (unsigned long long)query_bytes, (unsigned long long)ix->row_bytes);
   if (nq == 0) return 0;
   HIP_OK(hipSetDevice(ix->device));
   hipStream_t s = (hipStream_t)stream;  // null = the default stream
-  // enough slices to fill the chip: ~4 waves per CU over all queries
-  uint64_t want = ((uint64_t)ix->cu_count * 16 + nq - 1) / nq;
-  uint64_t maxs = (ix->nrows + 255) / 256;
-  uint32_t nslices = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxs, 1)));
   SearchCtx* c = ctx_for(ix, s);  // the slice buffer belongs to this index and stream
   if (!c) return -1;
-  DevBuf<uint64_t>& partial = c->partial;
-  HIP_OK(partial.alloc((size_t)nq * nslices * k));
   LinearArgs a{};
   a.rows = ix->rows.p;
   a.row_bytes = ix->row_bytes;
@@ -654,10 +654,39 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
   a.nq = nq;
   a.k = k;
   a.radius = radius;
-  a.partial = partial.p;
   a.out_ids = d_ids;
   a.out_dists = d_dists;
   a.out_n = d_n;
+  // Batches of queries: the query-tiled scan (128 queries per workgroup,
+  // packed FMA, scan_kernels.hip) over enough row parts for ~3 workgroups
+  // per CU slot; small batches keep the quad-per-row kernel below.
+  static const bool tiled = [] {
+    const char* v = getenv("NGT_AMD_LINEAR_TILED");
+    return !(v && atoi(v) == 0);
+  }();
+  if (tiled && nq >= 32 && ix->metric == NGT_AMD_DISTANCE_L2 && ix->otype == NGT_AMD_OBJECT_FLOAT && k <= 32 &&
+      ix->dp <= 256) {
+    const uint64_t qblocks = (nq + 127) / 128;
+    uint64_t nparts = ((uint64_t)ix->cu_count * 12 + qblocks - 1) / qblocks;
+    nparts = std::max<uint64_t>(1, std::min<uint64_t>(nparts, (ix->nrows + 1023) / 1024));
+    const uint64_t per = ((ix->nrows + nparts - 1) / nparts + 7) & ~7ull;
+    nparts = (ix->nrows + per - 1) / per;
+    HIP_OK(c->partial.alloc((size_t)nq * nparts * k));
+    a.partial = c->partial.p;
+    hipError_t e = launch_linear_scan(a, ix->metric, ix->otype, (uint32_t)nparts, (uint32_t)per, s);
+    if (e == hipSuccess) {
+      HIP_OK(launch_linear_merge(a, (uint32_t)nparts, s));
+      return 0;
+    }
+    if (e != hipErrorNotSupported) return fail("ngt_amd_linear_search_device: scan launch failed: %s",
+                                               hipGetErrorString(e));
+  }
+  // enough slices to fill the chip: ~4 waves per CU over all queries
+  uint64_t want = ((uint64_t)ix->cu_count * 16 + nq - 1) / nq;
+  uint64_t maxs = (ix->nrows + 255) / 256;
+  uint32_t nslices = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxs, 1)));
+  HIP_OK(c->partial.alloc((size_t)nq * nslices * k));
+  a.partial = c->partial.p;
   HIP_OK(launch_linear_search(a, ix->metric, ix->otype, nslices, s));
   return 0;
 }

@@ -192,6 +192,12 @@ hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint3
                                hipStream_t s);
 hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint32_t nslices,
                                 hipStream_t s);
+hipError_t launch_linear_merge(const LinearArgs& a, uint32_t nslices, hipStream_t s);
+// query-tiled exact scan (scan_kernels.hip): float L2, Dp <= 256, k <= 32;
+// hipErrorNotSupported otherwise.  Writes a.partial [nq][nparts][k].
+hipError_t launch_linear_scan(const LinearArgs& a, int metric, int otype, uint32_t nparts, uint32_t rows_per_part,
+                              hipStream_t s);
+size_t linear_scan_lds_bytes(uint32_t k, int dp);
 
 // ---- NGTQG (qg_kernels.hip) ------------------------------------------------
 struct QgLutArgs {

@@ -304,6 +304,9 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
                                         const uint32_t* d_seeds, const uint64_t* d_seed_off, uint32_t* d_ids,
                                         float* d_dists, uint32_t* d_n, uint64_t* d_counters, void* stream) {
   if (!ix || !prm || (!d_queries && nq)) return fail("ngt_amd_qg_search_device: bad arguments");
+  if (nq && query_bytes < ix->row_bytes)
+    return fail("ngt_amd_qg_search_device: query stride %llu < %llu bytes (queries are prepared rows of the padded dimension)",
+                (unsigned long long)query_bytes, (unsigned long long)ix->row_bytes);
   if (!ix->qg.has_graph) return fail("ngt_amd_qg_search: the index has no quantized graph");
   if (prm->k == 0) return fail("ngt_amd_qg_search: k must be > 0");
   if (nq == 0) return 0;

@@ -689,6 +689,10 @@ hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint
 #undef L_LIN
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  return launch_linear_merge(a, nslices, s);
+}
+
+hipError_t launch_linear_merge(const LinearArgs& a, uint32_t nslices, hipStream_t s) {
   const size_t lds2 = ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   hipLaunchKernelGGL(ngt_linear_merge_kernel, dim3(a.nq), dim3(64), lds2, s, a, nslices);
   return hipGetLastError();
