@@ -88,6 +88,8 @@ struct SearchCtx {
   DevBuf<uint8_t> lut;           // NGTQG: [nq][Me*16]
   DevBuf<float> scale, toff;
   DevBuf<uint64_t> partial;      // linear search: [nq][nslices][k] slice top-k
+  DevBuf<uint16_t> sqh, sql;     // matrix-core scan: queries in fragment order
+  DevBuf<float> shb;             // matrix-core scan: per-query filter base
   DevBuf<int> err;               // device error flag of the launches on this stream
   ~SearchCtx() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -172,6 +174,12 @@ struct ngt_amd_index {
   uint64_t row_bytes = 0;
   uint64_t nrows = 0;
   DevBuf<uint8_t> rows, valid;
+  uint64_t rows_version = 0;     // bumped whenever rows / valid change
+  struct {                       // matrix-core scan image of the rows (scan_mfma.hip)
+    DevBuf<uint16_t> rh, rl;
+    DevBuf<uint32_t> xmax;
+    uint64_t version = ~0ull;
+  } scan;
   std::vector<uint8_t> h_valid;
   std::vector<uint64_t> h_degree_nonzero;  // for isEmpty in getRandomSeeds
   DevBuf<uint64_t> edge_off;

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cfloat>
 #include <string>
 #include <vector>
@@ -104,6 +105,7 @@ extern "C" int ngt_amd_index_set_objects(ngt_amd_index* ix, const void* rows, ui
   HIP_OK(hipSetDevice(ix->device));
   HIP_OK(ix->rows.upload(static_cast<const uint8_t*>(rows), nrows * ix->row_bytes));
   ix->nrows = nrows;
+  ix->rows_version++;
   ix->h_valid.assign(nrows, 1);
   ix->h_valid[0] = 0;
   if (valid) ix->h_valid.assign(valid, valid + nrows);
@@ -119,6 +121,7 @@ extern "C" int ngt_amd_index_set_objects_device(ngt_amd_index* ix, const void* d
   ix->rows.n = nrows * ix->row_bytes;
   ix->rows.owned = false;
   ix->nrows = nrows;
+  ix->rows_version++;
   ix->h_valid.assign(nrows, 1);
   ix->h_valid[0] = 0;
   HIP_OK(ix->valid.upload(ix->h_valid.data(), nrows));
@@ -631,6 +634,155 @@ extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* pr
   return 0;
 }
 
+// Error-bound constants of the matrix-core filter (scan_mfma.hip, DESIGN.md
+// 4d): bf16 hi+lo splitting leaves < 3.1 * 2^-16 |q||x| of the dot product,
+// the fp32 accumulation of 3 dp + 16 terms < (3 dp + 16) 2^-24 of the sum of
+// magnitudes; both doubled, plus the comparator's own rounding (rho).
+static double scan_kappa(const ngt_amd_index* ix) {
+  const double dp = (double)ix->dp;
+  const double base = 3.2 * std::ldexp(1.0, -16) + (3.0 * dp + 64.0) * std::ldexp(1.0, -23);
+  return ix->metric == NGT_AMD_DISTANCE_COSINE ? 4.0 * base : 2.0 * base;
+}
+
+// The rows' bf16 hi/lo image in fragment order plus the norm column, built
+// once per version of the rows (first batch scan after set_objects).
+static int ensure_scan_rows(ngt_amd_index* ix, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (ix->scan.version == ix->rows_version) return 0;
+  const uint32_t ks = ix->dp / 16 + 1;
+  const uint64_t ntiles = (ix->nrows + 255) / 256;  // 256-row scan tiles
+  const size_t elems = (size_t)ntiles * 8 * ks * 512;
+  HIP_OK(ix->scan.rh.alloc(elems));
+  HIP_OK(ix->scan.rl.alloc(elems));
+  HIP_OK(ix->scan.xmax.alloc(1));
+  HIP_OK(hipMemsetAsync(ix->scan.xmax.p, 0, sizeof(uint32_t), s));
+  const double kappa = scan_kappa(ix);
+  ScanPrepArgs p{};
+  p.src = ix->rows.p;
+  p.stride = ix->row_bytes;
+  p.n = ix->nrows;
+  p.valid = ix->valid.p;
+  p.dp = (int)ix->dp;
+  p.ks = ks;
+  p.ntiles32 = ntiles * 8;
+  p.out_h = ix->scan.rh.p;
+  p.out_l = ix->scan.rl.p;
+  p.one_minus_kappa = (float)(1.0 - kappa);
+  p.kappa = (float)kappa;
+  p.xmax_bits = ix->scan.xmax.p;
+  HIP_OK(launch_scan_prep(p, ix->metric == NGT_AMD_DISTANCE_COSINE, false, s));
+  // other streams may scan as soon as the version is published
+  HIP_OK(hipStreamSynchronize(s));
+  ix->scan.version = ix->rows_version;
+  return 0;
+}
+
+static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hipStream_t s) {
+  if (ensure_scan_rows(ix, s)) return -1;
+  const bool cosine = ix->metric == NGT_AMD_DISTANCE_COSINE;
+  const uint32_t ks = ix->dp / 16 + 1;
+  const uint32_t mblocks = (a.nq + 127) / 128;  // 128 queries per workgroup
+  const uint64_t nqpad = (uint64_t)mblocks * 128;
+  HIP_OK(c->sqh.alloc((size_t)nqpad * ks * 16));
+  HIP_OK(c->sql.alloc((size_t)nqpad * ks * 16));
+  HIP_OK(c->shb.alloc(nqpad * 2));
+  const double kappa = scan_kappa(ix);
+  ScanPrepArgs p{};
+  p.src = a.queries;
+  p.stride = a.query_bytes;
+  p.n = a.nq;
+  p.n_pad = nqpad;
+  p.dp = (int)ix->dp;
+  p.ks = ks;
+  p.ntiles32 = nqpad / 32;
+  p.out_h = c->sqh.p;
+  p.out_l = c->sql.p;
+  p.one_minus_kappa = (float)(1.0 - kappa);
+  p.kappa = (float)kappa;
+  p.slack = std::ldexp(1.0f, -100);
+  p.xmax_bits = ix->scan.xmax.p;
+  p.hb = c->shb.p;
+  p.hm = c->shb.p + nqpad;
+  // bootstrap margin: two filter errors plus the comparator's rounding
+  const double rho = ((double)ix->dp + 64.0) * std::ldexp(1.0, -22);
+  p.kappa_boot = (float)(cosine ? 2.0 * kappa : kappa + rho);
+  HIP_OK(launch_scan_prep(p, cosine, true, s));
+
+  // parts: one workgroup per CU over all query blocks (a workgroup keeps
+  // its queries' k-lists for its whole part, so longer parts mean fewer
+  // list updates: each part costs ~k ln(rows / k) candidates per query)
+  static const int per_cu = [] {
+    const char* v = getenv("NGT_AMD_SCAN_WG_PER_CU");
+    return v ? std::max(1, atoi(v)) : 1;
+  }();
+  const uint32_t ntiles = (uint32_t)((ix->nrows + 255) / 256);
+  uint64_t nparts = (uint64_t)ix->cu_count * per_cu / mblocks;
+  nparts = std::max<uint64_t>(1, std::min<uint64_t>(nparts, ntiles));
+  const uint32_t per = (uint32_t)((ntiles + nparts - 1) / nparts);
+  nparts = (ntiles + per - 1) / per;
+  HIP_OK(c->partial.alloc((size_t)a.nq * nparts * a.k));
+  MfmaScanArgs m{};
+  m.rh = ix->scan.rh.p;
+  m.rl = ix->scan.rl.p;
+  m.qh = c->sqh.p;
+  m.ql = c->sql.p;
+  m.hb = c->shb.p;
+  m.hm = c->shb.p + nqpad;
+  m.rows = ix->rows.p;
+  m.row_bytes = ix->row_bytes;
+  m.queries = a.queries;
+  m.query_bytes = a.query_bytes;
+  m.nq = a.nq;
+  m.k = a.k;
+  m.ks = ks;
+  m.dp = (int)ix->dp;
+  m.mblocks = mblocks;
+  m.ntiles = ntiles;
+  m.tiles_per_part = per;
+  m.nparts = (uint32_t)nparts;
+  m.radius = a.radius;
+  if (cosine) {
+    m.scale = 1.0f;
+    m.t_init = a.radius < 0.0 || a.radius >= 3.0e38 ? INFINITY : (float)a.radius;
+  } else {
+    m.scale = (float)((1.0 + rho) * 0.5);
+    m.t_init = INFINITY;
+    if (a.radius >= 0.0 && a.radius < 3.0e38) {
+      // squared-sum bound of the radius (scan_sq_bound on the host)
+      float d = (float)a.radius;
+      uint32_t u;
+      memcpy(&u, &d, 4);
+      u++;
+      float dn;
+      memcpy(&dn, &u, 4);
+      float s2 = (float)((double)dn * (double)dn);
+      memcpy(&u, &s2, 4);
+      u++;
+      memcpy(&m.t_init, &u, 4);
+    }
+  }
+  m.partial = c->partial.p;
+  if (const char* v = getenv("NGT_AMD_SCAN_DBG")) m.dbg = (uint32_t)atoi(v);
+  static const bool stats = getenv("NGT_AMD_SCAN_STATS") != nullptr;
+  static DevBuf<unsigned long long> d_stats;
+  if (stats) {
+    HIP_OK(d_stats.alloc(4));
+    HIP_OK(hipMemsetAsync(d_stats.p, 0, 4 * sizeof(unsigned long long), s));
+    m.stats = d_stats.p;
+  }
+  a.partial = c->partial.p;
+  HIP_OK(launch_scan_mfma(m, ix->metric, s));
+  if (stats) {
+    unsigned long long h[4];
+    HIP_OK(hipMemcpyAsync(h, d_stats.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    fprintf(stderr, "scan_mfma: nq %u parts %u tiles/part %u wgs %u candidates %llu rounds %llu tiles_with_cand %llu\n",
+            a.nq, m.nparts, per, m.nparts * mblocks, h[0], h[1], h[2]);
+  }
+  HIP_OK(launch_linear_merge(a, (uint32_t)nparts, s));
+  return 0;
+}
+
 extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes,
                                             uint32_t nq, uint32_t k, double radius, uint32_t* d_ids,
                                             float* d_dists, uint32_t* d_n, void* stream) {
@@ -657,6 +809,16 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
   a.out_ids = d_ids;
   a.out_dists = d_dists;
   a.out_n = d_n;
+  // Batches of queries, L2 / Cosine: the matrix-core filtered scan
+  // (scan_mfma.hip) -- bf16 MFMA dot products with a proven error bound pick
+  // the candidates, the comparator recomputes them bit for bit.
+  static const bool use_mfma = [] {
+    const char* v = getenv("NGT_AMD_LINEAR_MFMA");
+    return !(v && atoi(v) == 0);
+  }();
+  if (use_mfma && nq >= 32 && ix->otype == NGT_AMD_OBJECT_FLOAT && k <= 16 &&
+      (ix->metric == NGT_AMD_DISTANCE_L2 || ix->metric == NGT_AMD_DISTANCE_COSINE))
+    return linear_search_mfma(ix, c, a, s);
   // Batches of queries: the query-tiled scan (128 queries per workgroup,
   // packed FMA, scan_kernels.hip) over enough row parts for ~3 workgroups
   // per CU slot; small batches keep the quad-per-row kernel below.

@@ -199,6 +199,49 @@ hipError_t launch_linear_scan(const LinearArgs& a, int metric, int otype, uint32
                               hipStream_t s);
 size_t linear_scan_lds_bytes(uint32_t k, int dp);
 
+// Matrix-core filtered exact scan (scan_mfma.hip).  Operands in fragment order:
+// [32-object tile][k-step][64 lanes][8 bf16], k-steps = dp/16 + 1 (the last one
+// carries the filter's norm column).
+struct ScanPrepArgs {
+  const uint8_t* src;            // float rows / prepared queries
+  uint64_t stride;               // bytes between objects
+  uint64_t n;                    // objects
+  uint64_t n_pad;                // queries: entries of hb to write
+  const uint8_t* valid;          // rows: [n] or null
+  int dp;
+  uint32_t ks;
+  uint64_t ntiles32;
+  uint16_t* out_h;
+  uint16_t* out_l;
+  float one_minus_kappa, kappa, slack, kappa_boot;
+  uint32_t* xmax_bits;           // rows: atomicMax target; queries: read
+  float* hb;                     // queries: [n_pad] filter base
+  float* hm;                     // queries: [n_pad] bootstrap margin
+};
+struct MfmaScanArgs {
+  const uint16_t* rh;
+  const uint16_t* rl;
+  const uint16_t* qh;
+  const uint16_t* ql;
+  const float* hb;
+  const float* hm;
+  const uint8_t* rows;
+  uint64_t row_bytes;
+  const uint8_t* queries;
+  uint64_t query_bytes;
+  uint32_t nq, k, ks;
+  int dp;
+  uint32_t mblocks, ntiles, tiles_per_part, nparts;
+  double radius;
+  float scale, t_init;
+  uint32_t dbg;                  // profiling knobs (NGT_AMD_SCAN_DBG): 1 no filter, 2 no processing
+  unsigned long long* stats;     // or null: [0] candidates, [1] processing rounds, [2] tiles with candidates
+  uint64_t* partial;             // [nq][nparts][k]
+};
+hipError_t launch_scan_prep(const ScanPrepArgs& a, bool cosine, bool query, hipStream_t s);
+hipError_t launch_scan_mfma(const MfmaScanArgs& a, int metric, hipStream_t s);
+size_t scan_mfma_lds_bytes(uint32_t k);
+
 // ---- NGTQG (qg_kernels.hip) ------------------------------------------------
 struct QgLutArgs {
   const uint8_t* queries;        // prepared float query rows (padded dp)

@@ -1,21 +1,27 @@
 #!/usr/bin/env python3
-"""Exact scan (ngt_amd_linear_search_device) on C2-shaped data: the tiled
-kernel (scan_kernels.hip) against the quad-per-row kernel (NGT_AMD_LINEAR_TILED=0
-in a child process) -- identical ids and distance bits -- and its time.
-usage: linear_check.py [n] [nq] [dim] [k]"""
+"""Exact scan (ngt_amd_linear_search_device) on C2/C3-shaped data: the
+matrix-core filtered scan (scan_mfma.hip, default), the query-tiled FMA scan
+(scan_kernels.hip, NGT_AMD_LINEAR_MFMA=0) and the quad-per-row kernel
+(NGT_AMD_LINEAR_MFMA=0 NGT_AMD_LINEAR_TILED=0), each in a child process --
+identical ids and distance bits required -- and their times.
+usage: linear_check.py [n] [nq] [dim] [k] [metric] [modes]
+  metric: l2 | cosine; modes: comma list of mfma,tiled,quad (default all
+  that support the metric)"""
 import json
 import os
 import subprocess
 import sys
-import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+ENVS = {"mfma": {}, "tiled": {"NGT_AMD_LINEAR_MFMA": "0"},
+        "quad": {"NGT_AMD_LINEAR_MFMA": "0", "NGT_AMD_LINEAR_TILED": "0"}}
 
-def run(n, nq, dim, k, out):
+
+def run(n, nq, dim, k, metric, out):
     import torch
     import bench
     from ngt_amd.device import DeviceIndex
@@ -25,7 +31,7 @@ def run(n, nq, dim, k, out):
     rows[1:, :dim] = torch.from_numpy(bench.splitmix_uniform(n, dim, bench.BASE_SEED)).to(dev)
     q = torch.zeros((nq, dp), dtype=torch.float32, device=dev)
     q[:, :dim] = torch.from_numpy(bench.splitmix_uniform(nq, dim, bench.BASE_SEED + 1)).to(dev)
-    ix = DeviceIndex("l2", "float", dim)
+    ix = DeviceIndex(metric, "float", dim)
     ix.set_objects_device(rows.data_ptr(), n + 1)
     oi = torch.zeros((nq, k), dtype=torch.int32, device=dev)
     od = torch.zeros((nq, k), dtype=torch.float32, device=dev)
@@ -45,22 +51,33 @@ def run(n, nq, dim, k, out):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
-        run(*[int(x) for x in sys.argv[2:6]], sys.argv[6])
+        run(*[int(x) for x in sys.argv[2:6]], sys.argv[6], sys.argv[7])
         sys.exit(0)
-    n, nq, dim, k = [int(x) for x in (sys.argv[1:5] + ["1000000", "10000", "128", "10"][len(sys.argv) - 1:])]
+    args = sys.argv[1:] + ["1000000", "10000", "128", "10", "l2", ""][len(sys.argv) - 1:]
+    n, nq, dim, k = [int(x) for x in args[:4]]
+    metric = args[4]
+    modes = [m for m in (args[5] or "mfma,tiled,quad").split(",") if m]
+    if metric != "l2":
+        modes = [m for m in modes if m != "tiled"]
     res = {}
-    for tiled in ("1", "0"):
-        out = "/tmp/lin_%s.npz" % tiled
-        env = dict(os.environ, NGT_AMD_LINEAR_TILED=tiled)
-        subprocess.check_call([sys.executable, __file__, "--child", str(n), str(nq), str(dim), str(k), out], env=env)
-        res[tiled] = np.load(out)
-    a, b = res["1"], res["0"]
-    same = (np.array_equal(a["n"], b["n"]) and np.array_equal(a["ids"], b["ids"]) and
-            np.array_equal(a["d"].view(np.uint32), b["d"].view(np.uint32)))
-    ms = float(np.min(a["ms"][1:]))
-    flop = 3.0 * n * nq * ((dim - 1) // 16 + 1) * 16
-    print(json.dumps({"n": n, "nq": nq, "dim": dim, "k": k, "identical": bool(same),
-                      "tiled_ms": a["ms"].tolist(), "quad_ms": b["ms"].tolist(),
-                      "tiled_tflops": flop / (ms * 1e-3) / 1e12, "frac_of_157": flop / (ms * 1e-3) / 157.3e12,
-                      "qps": nq / (ms * 1e-3)}))
+    for m in modes:
+        out = "/tmp/lin_%s.npz" % m
+        env = dict(os.environ, **ENVS[m])
+        subprocess.check_call([sys.executable, __file__, "--child", str(n), str(nq), str(dim), str(k), metric, out],
+                              env=env)
+        res[m] = np.load(out)
+    base = res[modes[-1]]
+    line = {"n": n, "nq": nq, "dim": dim, "k": k, "metric": metric}
+    same = True
+    flop = 3.0 * n * nq * ((dim - 1) // 16 + 1) * 16  # the comparator's sub + FMA per dimension
+    for m in modes:
+        a = res[m]
+        eq = (np.array_equal(a["n"], base["n"]) and np.array_equal(a["ids"], base["ids"]) and
+              np.array_equal(a["d"].view(np.uint32), base["d"].view(np.uint32)))
+        same = same and eq
+        ms = float(np.min(a["ms"][1:]))
+        line[m] = {"ms": a["ms"].tolist(), "identical_to_%s" % modes[-1]: bool(eq), "qps": nq / (ms * 1e-3),
+                   "effective_tflops": flop / (ms * 1e-3) / 1e12}
+    line["identical"] = bool(same)
+    print(json.dumps(line))
     sys.exit(0 if same else 1)
