@@ -297,6 +297,29 @@ def main():
     torch.cuda.synchronize()
     gt = gt_i.cpu().numpy()
     log("ground truth in %.1f s" % (time.time() - t0))
+    scan = None
+    if not shard and not qgm:
+        # the exact scan itself as a search method (recall 1.0): the batch
+        # linear search timed on the same resident queries
+        sms = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ix.linear_search_device(qdev.data_ptr(), dp * 4, NQ, K, gt_i.data_ptr(), gt_d.data_ptr(),
+                                    gt_n.data_ptr(), stream=stream)
+            e1.record()
+            torch.cuda.synchronize()
+            sms.append(e0.elapsed_time(e1))
+        if not np.array_equal(gt_i.cpu().numpy(), gt):
+            raise SystemExit("bench: exact scan not deterministic")
+        ms = float(min(sms))
+        macs = 3.0 * N * NQ * (dp + 16)  # bf16 hi/lo passes incl. the norm column
+        scan = {"qps": NQ / (ms * 1e-3), "ms": ms, "recall_at_10": 1.0,
+                "kernel": "ngt_scan_mfma_kernel (bf16 hi/lo MFMA filter + comparator recompute)" if K <= 16
+                else "ngt_linear_scan_l2f_kernel",
+                "effective_tflops": 3.0 * N * NQ * dp / (ms * 1e-3) / 1e12,
+                "mfma_bf16_frac": 2.0 * macs / (ms * 1e-3) / 2.5e15}
+        log("exact scan: %.2f ms per %d queries (%.0f QPS)" % (ms, NQ, scan["qps"]))
 
     seeds = random_seeds(N + 1, NQ, args.seed_size)
     d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
@@ -440,6 +463,8 @@ def main():
         torch.cuda.synchronize()
         gpu_out = (out_i.cpu().numpy().view(np.uint32), out_d.cpu().numpy(), out_n.cpu().numpy().view(np.uint32))
         cpu, parity = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric, gpu_out, full_cnt)
+        if scan is not None:
+            scan["oracle_sample"] = scan_sample_check(rows, qdev, metric, K, gt_i, gt_d, gt_n)
 
     if rank == 0:
         if args.mode == "exact" and not c3:
@@ -479,8 +504,10 @@ def main():
                        "seeds": "getRandomSeeds (%d)" % args.seed_size,
                        "distance_computations_per_query": float(c[:, 0].mean()),
                        "expansions_per_query": float(c[:, 2].mean()),
-                       "visited_set": {-2: "hbm-epochs+lds-filter, accepted ids only",
-                                       -1: "hbm-epochs+lds-filter"}.get(args.visited, "lds-hash"),
+                       "visited_set": ("hbm-epochs, every evaluated id (accepted-only and the LDS filter are "
+                                       "off for rows over 1 KiB)" if dp * 4 > 1024 and args.visited in (-1, -2) else
+                                       {-2: "hbm-epochs+lds-filter, accepted ids only",
+                                        -1: "hbm-epochs+lds-filter"}.get(args.visited, "lds-hash")),
                        "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world),
                        "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -490,6 +517,8 @@ def main():
             "parity_sample": parity,
             "sweep": sweep,
         }
+        if scan is not None:
+            line["exact_scan"] = scan
         if qgm:
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
@@ -668,6 +697,31 @@ def host_cpu():
     if os.environ.get("OMP_NUM_THREADS"):
         threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     return model, ncpu, max(1, threads)
+
+
+def scan_sample_check(rows, qdev, metric, k, gt_i, gt_d, gt_n, nsample=16):
+    """The exact scan's results on the first nsample queries against the
+    oracle's linearSearch restatement on all host cores: identical ids and
+    distance bits required (abort otherwise)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    t0 = time.time()
+    _, _, threads = host_cpu()
+    h_rows = rows.cpu().numpy()
+    h_q = qdev[:nsample].cpu().numpy()
+    oi, od, on = O.linear_search_batch(metric, h_rows, h_q, k, threads=threads, L=O.native_lib(O.host_isa()))
+    gi = gt_i[:nsample].cpu().numpy().view(np.uint32)
+    gd = gt_d[:nsample].cpu().numpy()
+    gn = gt_n[:nsample].cpu().numpy().view(np.uint32)
+    same = bool(np.array_equal(on, gn))
+    for q in range(nsample if same else 0):
+        m = int(on[q])
+        same = same and np.array_equal(oi[q, :m], gi[q, :m]) and np.array_equal(
+            od[q, :m].view(np.uint32), gd[q, :m].view(np.uint32))
+    if not same:
+        raise SystemExit("bench: exact scan differs from the oracle on the sample")
+    log("exact scan: %d-query oracle sample identical (%.1f s)" % (nsample, time.time() - t0))
+    return {"queries": nsample, "identical": True}
 
 
 def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_out, gpu_cnt):

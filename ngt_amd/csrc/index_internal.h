@@ -179,6 +179,7 @@ struct ngt_amd_index {
     DevBuf<uint16_t> rh, rl;
     DevBuf<uint32_t> xmax;
     uint64_t version = ~0ull;
+    int passes = 0;
   } scan;
   std::vector<uint8_t> h_valid;
   std::vector<uint64_t> h_degree_nonzero;  // for isEmpty in getRandomSeeds

@@ -635,20 +635,30 @@ extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* pr
 }
 
 // Error-bound constants of the matrix-core filter (scan_mfma.hip, DESIGN.md
-// 4d): bf16 hi+lo splitting leaves < 3.1 * 2^-16 |q||x| of the dot product,
-// the fp32 accumulation of 3 dp + 16 terms < (3 dp + 16) 2^-24 of the sum of
-// magnitudes; both doubled, plus the comparator's own rounding (rho).
-static double scan_kappa(const ngt_amd_index* ix) {
+// 4d): the bf16 hi+lo split (3 passes) leaves < 3.1 * 2^-16 |q||x| of the
+// dot product, bf16 alone (1 pass) < (2^-7 + 2^-16) |q||x|; the fp32
+// accumulation of P dp + 16 terms < (P dp + 16) 2^-24 of the sum of
+// magnitudes; both doubled (Cosine: quadrupled, it also absorbs the
+// normalization), plus the comparator's own rounding (rho) where used.
+static int scan_passes() {
+  static const int p = [] {
+    const char* v = getenv("NGT_AMD_SCAN_PASSES");
+    return v && atoi(v) == 1 ? 1 : 3;
+  }();
+  return p;
+}
+static double scan_kappa(const ngt_amd_index* ix, int passes) {
   const double dp = (double)ix->dp;
-  const double base = 3.2 * std::ldexp(1.0, -16) + (3.0 * dp + 64.0) * std::ldexp(1.0, -23);
+  const double split = passes == 3 ? 3.2 * std::ldexp(1.0, -16) : 1.02 * std::ldexp(1.0, -7);
+  const double base = split + (passes * dp + 64.0) * std::ldexp(1.0, -23);
   return ix->metric == NGT_AMD_DISTANCE_COSINE ? 4.0 * base : 2.0 * base;
 }
 
 // The rows' bf16 hi/lo image in fragment order plus the norm column, built
 // once per version of the rows (first batch scan after set_objects).
-static int ensure_scan_rows(ngt_amd_index* ix, hipStream_t s) {
+static int ensure_scan_rows(ngt_amd_index* ix, int passes, hipStream_t s) {
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (ix->scan.version == ix->rows_version) return 0;
+  if (ix->scan.version == ix->rows_version && ix->scan.passes == passes) return 0;
   const uint32_t ks = ix->dp / 16 + 1;
   const uint64_t ntiles = (ix->nrows + 255) / 256;  // 256-row scan tiles
   const size_t elems = (size_t)ntiles * 8 * ks * 512;
@@ -656,7 +666,7 @@ static int ensure_scan_rows(ngt_amd_index* ix, hipStream_t s) {
   HIP_OK(ix->scan.rl.alloc(elems));
   HIP_OK(ix->scan.xmax.alloc(1));
   HIP_OK(hipMemsetAsync(ix->scan.xmax.p, 0, sizeof(uint32_t), s));
-  const double kappa = scan_kappa(ix);
+  const double kappa = scan_kappa(ix, passes);
   ScanPrepArgs p{};
   p.src = ix->rows.p;
   p.stride = ix->row_bytes;
@@ -674,11 +684,13 @@ static int ensure_scan_rows(ngt_amd_index* ix, hipStream_t s) {
   // other streams may scan as soon as the version is published
   HIP_OK(hipStreamSynchronize(s));
   ix->scan.version = ix->rows_version;
+  ix->scan.passes = passes;
   return 0;
 }
 
 static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hipStream_t s) {
-  if (ensure_scan_rows(ix, s)) return -1;
+  const int passes = scan_passes();
+  if (ensure_scan_rows(ix, passes, s)) return -1;
   const bool cosine = ix->metric == NGT_AMD_DISTANCE_COSINE;
   const uint32_t ks = ix->dp / 16 + 1;
   const uint32_t mblocks = (a.nq + 127) / 128;  // 128 queries per workgroup
@@ -686,7 +698,7 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
   HIP_OK(c->sqh.alloc((size_t)nqpad * ks * 16));
   HIP_OK(c->sql.alloc((size_t)nqpad * ks * 16));
   HIP_OK(c->shb.alloc(nqpad * 2));
-  const double kappa = scan_kappa(ix);
+  const double kappa = scan_kappa(ix, passes);
   ScanPrepArgs p{};
   p.src = a.queries;
   p.stride = a.query_bytes;
@@ -771,7 +783,7 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
     m.stats = d_stats.p;
   }
   a.partial = c->partial.p;
-  HIP_OK(launch_scan_mfma(m, ix->metric, s));
+  HIP_OK(launch_scan_mfma(m, ix->metric, passes, s));
   if (stats) {
     unsigned long long h[4];
     HIP_OK(hipMemcpyAsync(h, d_stats.p, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -239,7 +239,7 @@ struct MfmaScanArgs {
   uint64_t* partial;             // [nq][nparts][k]
 };
 hipError_t launch_scan_prep(const ScanPrepArgs& a, bool cosine, bool query, hipStream_t s);
-hipError_t launch_scan_mfma(const MfmaScanArgs& a, int metric, hipStream_t s);
+hipError_t launch_scan_mfma(const MfmaScanArgs& a, int metric, int passes, hipStream_t s);
 size_t scan_mfma_lds_bytes(uint32_t k);
 
 // ---- NGTQG (qg_kernels.hip) ------------------------------------------------

@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(64) ngt_scan_prep_kernel(ScanPrepArgs a) {
 // staging ring's LDS-DMA loads (vmcnt(0)); the ring is waited for by count.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int M>
+template <int M, int P>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 ngt_scan_mfma_kernel(MfmaScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -354,10 +354,12 @@ ngt_scan_mfma_kernel(MfmaScanArgs a) {
     const size_t qo = (((size_t)mb * 4 + w) * ks + s) * 512 + (size_t)lane * 8;
     __builtin_amdgcn_global_load_lds((const void*)(a.rh + ro0), (lds_ptr)(base), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(a.rh + ro1), (lds_ptr)(base + 4096), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(a.rl + ro0), (lds_ptr)(base + 8192), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(a.rl + ro1), (lds_ptr)(base + 12288), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(a.qh + qo), (lds_ptr)(base + 16384), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(a.ql + qo), (lds_ptr)(base + 20480), 16, 0, 0);
+    if (P == 3) {  // the lo parts
+      __builtin_amdgcn_global_load_lds((const void*)(a.rl + ro0), (lds_ptr)(base + 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(a.rl + ro1), (lds_ptr)(base + 12288), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(a.ql + qo), (lds_ptr)(base + 20480), 16, 0, 0);
+    }
   };
 
   f32x16 acc[4][2];
@@ -376,10 +378,11 @@ ngt_scan_mfma_kernel(MfmaScanArgs a) {
   const int rsh = 4 * (lane >> 5);
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t rt = t0 + g / ks, s = g - (g / ks) * ks;
-    // k-step g has landed once at most k-steps g+1, g+2 (6 loads each) are
+    // k-step g has landed once at most k-steps g+1, g+2 (2P loads each) are
     // outstanding; the barrier publishes every wave's blocks and retires the
     // reads of slot (g + 3) % 4, which is refilled right after
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    if (P == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     lds_barrier();
     issue(g + 3);
     // hi x hi + hi x lo + lo x hi (the norm column's lo parts are 0)
@@ -389,20 +392,22 @@ ngt_scan_mfma_kernel(MfmaScanArgs a) {
 #pragma unroll
       for (int mt = 0; mt < 4; mt++) {
         ah[mt] = *reinterpret_cast<const bf16x8*>(sb + (wr * 4 + mt) * 1024);
-        al[mt] = *reinterpret_cast<const bf16x8*>(sb + 8192 + (wr * 4 + mt) * 1024);
+        if (P == 3) al[mt] = *reinterpret_cast<const bf16x8*>(sb + 8192 + (wr * 4 + mt) * 1024);
       }
 #pragma unroll
       for (int nt = 0; nt < 2; nt++) {
         bh[nt] = *reinterpret_cast<const bf16x8*>(sb + 16384 + (wq * 2 + nt) * 1024);
-        bl[nt] = *reinterpret_cast<const bf16x8*>(sb + 20480 + (wq * 2 + nt) * 1024);
+        if (P == 3) bl[nt] = *reinterpret_cast<const bf16x8*>(sb + 20480 + (wq * 2 + nt) * 1024);
       }
 #pragma unroll
       for (int mt = 0; mt < 4; mt++)
 #pragma unroll
         for (int nt = 0; nt < 2; nt++) {
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+          if (P == 3) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+          }
         }
     }
     if (s + 1 < ks) continue;
@@ -597,28 +602,25 @@ hipError_t launch_scan_prep(const ScanPrepArgs& a, bool cosine, bool query, hipS
   return hipGetLastError();
 }
 
-hipError_t launch_scan_mfma(const MfmaScanArgs& a, int metric, hipStream_t s) {
+template <int M, int P>
+static void launch_scan_mfma_t(const MfmaScanArgs& a, size_t lds, uint32_t grid, hipStream_t s) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)ngt_scan_mfma_kernel<M, P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((ngt_scan_mfma_kernel<M, P>), dim3(grid), dim3(256), lds, s, a);
+}
+
+hipError_t launch_scan_mfma(const MfmaScanArgs& a, int metric, int passes, hipStream_t s) {
   const size_t lds = scan_mfma_lds_bytes(a.k);
   const uint32_t grid = a.nparts * a.mblocks;
-  if (metric == kL2) {
-    static bool attr = [] {
-      (void)hipFuncSetAttribute((const void*)ngt_scan_mfma_kernel<kL2>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      return true;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL((ngt_scan_mfma_kernel<kL2>), dim3(grid), dim3(256), lds, s, a);
-  } else if (metric == kCosine) {
-    static bool attr = [] {
-      (void)hipFuncSetAttribute((const void*)ngt_scan_mfma_kernel<kCosine>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      return true;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL((ngt_scan_mfma_kernel<kCosine>), dim3(grid), dim3(256), lds, s, a);
-  } else {
-    return hipErrorNotSupported;
-  }
+  if (metric == kL2 && passes == 3) launch_scan_mfma_t<kL2, 3>(a, lds, grid, s);
+  else if (metric == kL2 && passes == 1) launch_scan_mfma_t<kL2, 1>(a, lds, grid, s);
+  else if (metric == kCosine && passes == 3) launch_scan_mfma_t<kCosine, 3>(a, lds, grid, s);
+  else if (metric == kCosine && passes == 1) launch_scan_mfma_t<kCosine, 1>(a, lds, grid, s);
+  else return hipErrorNotSupported;
   return hipGetLastError();
 }
 
