@@ -444,7 +444,7 @@ def main():
         alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + NQ * (dp * 4 + K * 8)
         kname = "ngt_graph_search_kernel"
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = measured_traffic(args.mode, args.config, graph, chosen, args.visited)
+    traffic, tentry = measured_traffic(args.mode, args.config, graph, chosen, args.visited)
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
         tot = c[:, [5, 6, 7, 3]].mean(0)
         log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
@@ -519,6 +519,14 @@ def main():
         }
         if scan is not None:
             line["exact_scan"] = scan
+        cn = tentry.get("counters_per_launch")
+        if cn:
+            # PMC evidence for what bounds the kernel (profiles/traffic.json):
+            # share of wave-cycles issuing VALU, actual HBM bytes / algorithmic
+            line["roofline"]["counters"] = {
+                "source": tentry.get("source", ""), "SQ_INSTS_VALU": cn["SQ_INSTS_VALU"],
+                "valu_wave_cycle_frac": cn["SQ_ACTIVE_INST_VALU"] / cn["SQ_WAVE_CYCLES"],
+                "traffic_over_algorithmic": traffic / alg_bytes}
         if qgm:
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
@@ -539,17 +547,17 @@ def measured_traffic(mode, config, graph, eps, visited):
     exact workload and epsilon; NGT_BENCH_TRAFFIC_BYTES overrides; else None."""
     tf = os.environ.get("NGT_BENCH_TRAFFIC_BYTES")
     if tf:
-        return float(tf)
+        return float(tf), {}
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
-        return None
+        return None, {}
     for e in entries:
         if (e.get("mode", "exact") == mode and e.get("config", "c2") == config and e["graph"] == graph
                 and e.get("visited", -1) == visited and abs(e["epsilon"] - eps) < 1e-7):
-            return float(e["traffic_bytes"])
-    return None
+            return float(e["traffic_bytes"]), e
+    return None, {}
 
 
 def write_ngt_index(path, rows, offsets, edges, dim):

@@ -90,6 +90,7 @@ struct SearchCtx {
   DevBuf<uint64_t> partial;      // linear search: [nq][nslices][k] slice top-k
   DevBuf<uint16_t> sqh, sql;     // matrix-core scan: queries in fragment order
   DevBuf<float> shb;             // matrix-core scan: per-query filter base
+  DevBuf<uint64_t> gthr;         // matrix-core scan: per-query k-th key shared by the parts
   DevBuf<int> err;               // device error flag of the launches on this stream
   ~SearchCtx() {
     if (ev0) (void)hipEventDestroy(ev0);

@@ -720,19 +720,25 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
   p.kappa_boot = (float)(cosine ? 2.0 * kappa : kappa + rho);
   HIP_OK(launch_scan_prep(p, cosine, true, s));
 
-  // parts: one workgroup per CU over all query blocks (a workgroup keeps
-  // its queries' k-lists for its whole part, so longer parts mean fewer
-  // list updates: each part costs ~k ln(rows / k) candidates per query)
-  static const int per_cu = [] {
-    const char* v = getenv("NGT_AMD_SCAN_WG_PER_CU");
-    return v ? std::max(1, atoi(v)) : 1;
-  }();
+  // Launches of at most one workgroup per CU.  Default: one launch, every
+  // query block x floor(CUs / blocks) parts (a workgroup keeps its queries'
+  // k-lists for its whole part; each part costs ~k ln(rows / k) candidates per
+  // query, so few long parts).  NGT_AMD_SCAN_XCD=1: launches of up to CUs / 8
+  // query blocks with 8 r parts, part p on XCD p % 8, so the workgroups that
+  // stream one part share that XCD's L2 (less fabric traffic, more parts).
   const uint32_t ntiles = (uint32_t)((ix->nrows + 255) / 256);
-  uint64_t nparts = (uint64_t)ix->cu_count * per_cu / mblocks;
-  nparts = std::max<uint64_t>(1, std::min<uint64_t>(nparts, ntiles));
-  const uint32_t per = (uint32_t)((ntiles + nparts - 1) / nparts);
-  nparts = (ntiles + per - 1) / per;
-  HIP_OK(c->partial.alloc((size_t)a.nq * nparts * a.k));
+  static const bool xcd = [] {
+    const char* v = getenv("NGT_AMD_SCAN_XCD");
+    return v && atoi(v) != 0;
+  }();
+  const uint32_t per_launch = xcd ? std::max(1, ix->cu_count / 8) : mblocks;
+  auto parts_of = [&](uint32_t mbc) -> uint32_t {
+    if (xcd) return 8 * std::max<uint32_t>(1, per_launch / mbc);
+    uint32_t np = std::max<uint32_t>(1, (uint32_t)ix->cu_count / mbc);
+    np = std::min(np, ntiles);
+    const uint32_t per = (ntiles + np - 1) / np;
+    return (ntiles + per - 1) / per;
+  };
   MfmaScanArgs m{};
   m.rh = ix->scan.rh.p;
   m.rl = ix->scan.rl.p;
@@ -748,10 +754,7 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
   m.k = a.k;
   m.ks = ks;
   m.dp = (int)ix->dp;
-  m.mblocks = mblocks;
   m.ntiles = ntiles;
-  m.tiles_per_part = per;
-  m.nparts = (uint32_t)nparts;
   m.radius = a.radius;
   if (cosine) {
     m.scale = 1.0f;
@@ -773,7 +776,6 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
       memcpy(&m.t_init, &u, 4);
     }
   }
-  m.partial = c->partial.p;
   if (const char* v = getenv("NGT_AMD_SCAN_DBG")) m.dbg = (uint32_t)atoi(v);
   static const bool stats = getenv("NGT_AMD_SCAN_STATS") != nullptr;
   static DevBuf<unsigned long long> d_stats;
@@ -782,16 +784,45 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
     HIP_OK(hipMemsetAsync(d_stats.p, 0, 4 * sizeof(unsigned long long), s));
     m.stats = d_stats.p;
   }
-  a.partial = c->partial.p;
-  HIP_OK(launch_scan_mfma(m, ix->metric, passes, s));
+  HIP_OK(c->gthr.alloc(a.nq));
+  HIP_OK(hipMemsetAsync(c->gthr.p, 0xff, (size_t)a.nq * sizeof(uint64_t), s));
+  m.gthr = reinterpret_cast<unsigned long long*>(c->gthr.p);
+  // partial lists of every launch, back to back
+  size_t partial_total = 0;
+  for (uint32_t mb0 = 0; mb0 < mblocks; mb0 += per_launch) {
+    const uint32_t mbc = std::min(per_launch, mblocks - mb0);
+    const uint32_t nqc = std::min<uint32_t>(a.nq - mb0 * 128, mbc * 128);
+    partial_total += (size_t)nqc * parts_of(mbc) * a.k;
+  }
+  HIP_OK(c->partial.alloc(partial_total));
+  size_t poff = 0;
+  m.xcd = xcd ? 1 : 0;
+  for (uint32_t mb0 = 0; mb0 < mblocks; mb0 += per_launch) {
+    const uint32_t mbc = std::min(per_launch, mblocks - mb0);
+    const uint32_t nqc = std::min<uint32_t>(a.nq - mb0 * 128, mbc * 128);
+    const uint32_t nparts = parts_of(mbc);
+    m.mb0 = mb0;
+    m.mblocks = mbc;
+    m.nparts = nparts;
+    m.tiles_per_part = (ntiles + nparts - 1) / nparts;
+    m.partial = c->partial.p + poff;
+    HIP_OK(launch_scan_mfma(m, ix->metric, passes, s));
+    LinearArgs ac = a;
+    ac.nq = nqc;
+    ac.partial = m.partial;
+    ac.out_ids = a.out_ids + (size_t)mb0 * 128 * a.k;
+    ac.out_dists = a.out_dists + (size_t)mb0 * 128 * a.k;
+    ac.out_n = a.out_n + (size_t)mb0 * 128;
+    HIP_OK(launch_linear_merge(ac, nparts, s));
+    poff += (size_t)nqc * nparts * a.k;
+  }
   if (stats) {
     unsigned long long h[4];
     HIP_OK(hipMemcpyAsync(h, d_stats.p, sizeof(h), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    fprintf(stderr, "scan_mfma: nq %u parts %u tiles/part %u wgs %u candidates %llu rounds %llu tiles_with_cand %llu\n",
-            a.nq, m.nparts, per, m.nparts * mblocks, h[0], h[1], h[2]);
+    fprintf(stderr, "scan_mfma: nq %u launches %u candidates %llu rounds %llu process_requests %llu\n", a.nq,
+            (mblocks + per_launch - 1) / per_launch, h[0], h[1], h[2]);
   }
-  HIP_OK(launch_linear_merge(a, (uint32_t)nparts, s));
   return 0;
 }
 

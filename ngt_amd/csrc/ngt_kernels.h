@@ -231,11 +231,13 @@ struct MfmaScanArgs {
   uint64_t query_bytes;
   uint32_t nq, k, ks;
   int dp;
-  uint32_t mblocks, ntiles, tiles_per_part, nparts;
+  uint32_t mb0, mblocks, ntiles, tiles_per_part, nparts;  // this launch: query blocks mb0 .. + mblocks
+  uint32_t xcd;                  // parts a multiple of 8, part p on XCD p % 8
   double radius;
   float scale, t_init;
   uint32_t dbg;                  // profiling knobs (NGT_AMD_SCAN_DBG): 1 no filter, 2 no processing
   unsigned long long* stats;     // or null: [0] candidates, [1] processing rounds, [2] tiles with candidates
+  unsigned long long* gthr;      // [nq] smallest k-th key over the parts (all ones at launch)
   uint64_t* partial;             // [nq][nparts][k]
 };
 hipError_t launch_scan_prep(const ScanPrepArgs& a, bool cosine, bool query, hipStream_t s);

@@ -266,8 +266,12 @@ ngt_scan_mfma_kernel(MfmaScanArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w & 1, wq = w >> 1;
-  const uint32_t mb = blockIdx.x % a.mblocks;
-  const uint32_t part = blockIdx.x / a.mblocks;
+  // the launch covers query blocks mb0 .. mb0 + mblocks - 1; its parts are
+  // a multiple of 8 and part p runs on XCD p % 8 (blockIdx % 8 picks the
+  // XCD), so the workgroups streaming one part share that XCD's L2
+  const uint32_t slot = a.xcd ? blockIdx.x >> 3 : blockIdx.x;
+  const uint32_t mb = a.mb0 + slot % a.mblocks;
+  const uint32_t part = a.xcd ? (slot / a.mblocks) * 8 + (blockIdx.x & 7) : slot / a.mblocks;
   const uint32_t q0 = mb * kMxQ;
   const uint32_t t0 = part * a.tiles_per_part;
   uint32_t t1 = t0 + a.tiles_per_part;
@@ -327,13 +331,21 @@ ngt_scan_mfma_kernel(MfmaScanArgs a) {
       }
       if (a.stats) atomicAdd(&a.stats[0], (unsigned long long)n);
       pc[tid] = 0;
-      if (th != thr[tid]) {
-        thr[tid] = th;
-        const float kd = key_dist(th);
+      thr[tid] = th;
+      cnt[tid] = c;
+    }
+    if (tid < kMxQ && q0 + tid < a.nq) {
+      // every part's k-th key bounds the query's global k-th key: publish
+      // this part's, take the smallest over the parts for the filter
+      const uint64_t th = thr[tid];
+      const uint64_t g = __hip_atomic_fetch_min(a.gthr + q0 + tid, (unsigned long long)th, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t best = g < th ? g : th;
+      if (best != ~0ull) {
+        const float kd = key_dist(best);
         const float tv = M == kL2 ? fminf(a.t_init, scan_sq_bound(kd)) : fminf(a.t_init, kd);
         H[tid] = fmaxf(H[tid], HB[tid] - a.scale * tv);
       }
-      cnt[tid] = c;
     }
     if (a.stats && tid == 0) atomicAdd(&a.stats[1], 1ull);
     lds_barrier();
@@ -580,7 +592,8 @@ ngt_scan_mfma_kernel(MfmaScanArgs a) {
   for (uint32_t i = tid; i < (uint32_t)kMxQ * k; i += 256) {
     const uint32_t ql = i / k, r = i - ql * k;
     const uint32_t qi = q0 + ql;
-    if (qi < a.nq) a.partial[((uint64_t)qi * a.nparts + part) * k + r] = r < cnt[ql] ? lists[i] : ~0ull;
+    if (qi < a.nq)
+      a.partial[((uint64_t)(qi - a.mb0 * kMxQ) * a.nparts + part) * k + r] = r < cnt[ql] ? lists[i] : ~0ull;
   }
 }
 
