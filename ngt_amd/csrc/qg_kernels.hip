@@ -29,6 +29,11 @@
 #include "ngt_kernels.h"
 #include "search_common.h"
 
+// 1: the previous all-VALU cross-lane sum (v_perm packing + reduce-scatter)
+#ifndef NGT_AMD_QG_VALU_REDUCE
+#define NGT_AMD_QG_VALU_REDUCE 0
+#endif
+
 namespace ngt_amd {
 
 // ---------------------------------------------------------------------------
@@ -290,9 +295,84 @@ __device__ __forceinline__ void load_lane_lut(LaneLut<PPL>& L, const uint8_t* lu
       a = src[0];
       b = src[1];
     }
+#if !NGT_AMD_QG_VALU_REDUCE
+    // table bytes as signed v - 128 for the i8 MFMA sum (adc_sum_mfma);
+    // padding lanes stay 0 and contribute nothing
+    if (p < npairs) {
+      a.x ^= 0x80808080u; a.y ^= 0x80808080u; a.z ^= 0x80808080u; a.w ^= 0x80808080u;
+      b.x ^= 0x80808080u; b.y ^= 0x80808080u; b.z ^= 0x80808080u; b.w ^= 0x80808080u;
+    }
+#endif
     L.t[s][0] = a.x; L.t[s][1] = a.y; L.t[s][2] = a.z; L.t[s][3] = a.w;
     L.t[s][4] = b.x; L.t[s][5] = b.y; L.t[s][6] = b.z; L.t[s][7] = b.w;
   }
+}
+
+// ---------------------------------------------------------------------------
+// The cross-lane sum on the matrix cores.  A block's looked-up bytes sit
+// lane = subspace pair, byte = object; the sum over subspaces is a sum over
+// lanes.  One v_mfma_i32_16x16x64_i8 per subspace (even: e0..e3, odd:
+// o0..o3) takes a lane's 16 looked-up bytes as its A fragment (row = lane &
+// 15, k = the lane's 16 bytes within lane group lane >> 4) against a constant
+// one-hot B whose byte t in column j is 1 iff byte t holds object j, so
+// C[i][j] = sum over the four lanes {i, 16+i, 32+i, 48+i} of object j's
+// bytes; A and B share the k map, so that map's details do not matter.  The
+// 16 rows of C (4 registers x 4 lane groups) are then folded: three adds and
+// two lane swaps.  The table bytes are stored as v ^ 0x80 = v - 128 (signed
+// i8), so the exact int32 sum is S - 128 * Me; adc_epilogue_total adds it
+// back.  Replaces the 16 packing v_perm and ~35 reduce-scatter ops per block.
+typedef int qg_i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ qg_i32x4 qg_onehot_b() {
+  const uint32_t j = (uint32_t)lane_id() & 15u;
+  qg_i32x4 b;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      // dword d of (e0, e1, e2, e3): objects 2t, 2t + 1, 8 + 2t, 9 + 2t
+      const uint32_t obj = (uint32_t)((d >> 1) * 8 + 2 * t + (d & 1));
+      if (obj == j) w |= 1u << (8 * t);
+    }
+    b[d] = (int)w;
+  }
+  return b;
+}
+
+template <int PPL>
+__device__ __forceinline__ uint32_t adc_sum_mfma(const LaneLut<PPL>& L, const uint4 (&c)[PPL], qg_i32x4 onehot) {
+  qg_i32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < PPL; s++) {
+    const uint32_t* t = L.t[s];
+    qg_i32x4 ev, od;
+    ev[0] = (int)lut16<0>(c[s].x, t[0], t[1], t[2], t[3]);  // objects 0,2,4,6
+    ev[1] = (int)lut16<4>(c[s].x, t[0], t[1], t[2], t[3]);  // 1,3,5,7
+    ev[2] = (int)lut16<0>(c[s].y, t[0], t[1], t[2], t[3]);  // 8,...,14
+    ev[3] = (int)lut16<4>(c[s].y, t[0], t[1], t[2], t[3]);  // 9,...,15
+    od[0] = (int)lut16<0>(c[s].z, t[4], t[5], t[6], t[7]);
+    od[1] = (int)lut16<4>(c[s].z, t[4], t[5], t[6], t[7]);
+    od[2] = (int)lut16<0>(c[s].w, t[4], t[5], t[6], t[7]);
+    od[3] = (int)lut16<4>(c[s].w, t[4], t[5], t[6], t[7]);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ev, onehot, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(od, onehot, acc, 0, 0, 0);
+  }
+  uint32_t r = (uint32_t)(acc[0] + acc[1]) + (uint32_t)(acc[2] + acc[3]);
+  {
+    const auto x = __builtin_amdgcn_permlane32_swap(r, r, false, false);  // lane ^ 32
+    r = x[0] + x[1];
+  }
+  {
+    const auto x = __builtin_amdgcn_permlane16_swap(r, r, false, false);  // lane ^ 16
+    r = x[0] + x[1];
+  }
+  return r;  // every lane: signed sum of object lane & 15
+}
+
+// sqrtf(fmaf(E + O, scale, totalOffset)) from the signed MFMA sum.
+__device__ __forceinline__ float adc_epilogue_total(uint32_t ssum, uint32_t Me, float scale, float toff) {
+  return sqrtf(__builtin_fmaf((float)(ssum + 128u * Me), scale, toff));
 }
 
 // Packed per-object partial sums of one lane for one block: v[o] =
@@ -395,6 +475,8 @@ __device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* c
   const uint32_t npairs = Me >> 1;
   const uint32_t nb = n == 0 ? 0 : (n - 1) / 16 + 1;
   const uint64_t blk = (uint64_t)8 * Me;
+  const qg_i32x4 onehot = qg_onehot_b();
+  (void)onehot;
   // blocks whose loads are in flight together (bounded by VGPRs)
   constexpr int NBF = PPL >= 4 ? 1 : (PPL == 2 ? 2 : 4);
   for (uint32_t b0 = 0; b0 < nb; b0 += NBF) {
@@ -412,11 +494,17 @@ __device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* c
 #pragma unroll
     for (int j = 0; j < NBF; j++) {
       if (b0 + j < nb) {
+#if NGT_AMD_QG_VALU_REDUCE
         uint32_t v[16];
         block_partials<PPL>(L, c[j], v);
         const uint32_t r = reduce_scatter16(v);
         const uint32_t o = (b0 + j) * 16 + qg_obj_of_lane(lane);
         if ((lane & 3) == 0 && o < n) dists[o] = adc_epilogue(r, scale, toff);
+#else
+        const uint32_t r = adc_sum_mfma<PPL>(L, c[j], onehot);
+        const uint32_t o = (b0 + j) * 16 + ((uint32_t)lane & 15u);
+        if (lane < 16 && o < n) dists[o] = adc_epilogue_total(r, Me, scale, toff);
+#endif
       }
     }
   }
@@ -442,6 +530,8 @@ __device__ __forceinline__ uint32_t ids_and_adc(const LaneLut<PPL>& L, const uin
   const uint32_t npairs = Me >> 1;
   const uint64_t blk = (uint64_t)8 * Me;
   const uint32_t nbs = id_stride >> 4;
+  const qg_i32x4 onehot = qg_onehot_b();
+  (void)onehot;
   uint4 c[NB][PPL];
 #pragma unroll
   for (int j = 0; j < NB; j++) {
@@ -483,11 +573,17 @@ __device__ __forceinline__ uint32_t ids_and_adc(const LaneLut<PPL>& L, const uin
 #pragma unroll
   for (int j = 0; j < NB; j++) {
     if ((uint32_t)j < nb) {
+#if NGT_AMD_QG_VALU_REDUCE
       uint32_t v[16];
       block_partials<PPL>(L, c[j], v);
       const uint32_t r = reduce_scatter16(v);
       const uint32_t o = (uint32_t)j * 16 + qg_obj_of_lane(lane);
       if ((lane & 3) == 0 && o < deg) dists[o] = adc_epilogue(r, scale, toff);
+#else
+      const uint32_t r = adc_sum_mfma<PPL>(L, c[j], onehot);
+      const uint32_t o = (uint32_t)j * 16 + ((uint32_t)lane & 15u);
+      if (lane < 16 && o < deg) dists[o] = adc_epilogue_total(r, Me, scale, toff);
+#endif
     }
   }
   seen[0] = seen[1] = 0;

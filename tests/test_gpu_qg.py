@@ -340,3 +340,73 @@ def test_ngtqg_quantize_capi(tmp_path):
     rec = np.mean([len(set(bi[i, :bn[i]].tolist()) & set(li[i, :ln[i]].tolist())) / 10.0 for i in range(len(qs))])
     assert rec >= 0.9, rec
     qi.close()
+
+
+def _synthetic_qg(dim, n, maxe, seed):
+    """A QG index over n random rows of `dim` floats (dsub 1 => M = dim): a
+    kNN graph, random codebooks and nearest-centroid codes, in both the
+    oracle's form (read_qg's dict) and the device's."""
+    rng = np.random.default_rng(seed)
+    dp = F.padded_dim(dim)
+    rows = np.zeros((n + 1, dp), np.float32)
+    rows[1:, :dim] = rng.random((n, dim), dtype=np.float32)
+    x = rows[1:, :dim].astype(np.float64)
+    sq = (x * x).sum(1)
+    d2 = sq[:, None] + sq[None, :] - 2.0 * x @ x.T
+    np.fill_diagonal(d2, np.inf)
+    nn = np.argsort(d2, axis=1, kind="stable")[:, :maxe] + 1
+    offs = np.zeros(n + 2, np.uint64)
+    offs[2:] = np.cumsum(np.full(n, maxe, np.uint64))
+    ids = nn.reshape(-1).astype(np.uint32)
+    M = dim
+    local = np.zeros((M, 17, 1), np.float32)
+    local[:, 1:, 0] = rng.random((M, 16), dtype=np.float32)
+    codes = np.abs(rows[:, :dim, None] - local[None, :, 1:, 0]).argmin(2).astype(np.uint8)  # [n+1, M]
+    me = (M + 1) // 2 * 2
+    qoff = np.zeros(n + 2, np.uint64)
+    code_off = np.zeros(n + 2, np.uint64)
+    blobs = []
+    for v in range(n + 1):
+        e = ids[int(offs[v]):int(offs[v + 1])]
+        qoff[v + 1] = qoff[v] + len(e)
+        if len(e) == 0:
+            code_off[v + 1] = code_off[v]
+            continue
+        nb = (len(e) - 1) // 16 + 1
+        lc = np.zeros((nb * 16, M), np.uint8)
+        lc[:len(e)] = codes[e]
+        st = np.zeros((nb, me, 16), np.uint8)
+        st[:, :M, :] = lc.reshape(nb, 16, M).transpose(0, 2, 1)
+        st = st.reshape(-1)
+        c = (st[0::2] | (st[1::2] << 4)).astype(np.uint8).tobytes()
+        blobs.append(c)
+        code_off[v + 1] = code_off[v] + len(c)
+    qg = {"dim": dim, "M": M, "dsub": 1, "global": np.zeros(dp, np.float32), "local": local,
+          "qoff": qoff, "qids": ids, "code_off": code_off, "codes": np.frombuffer(b"".join(blobs), np.uint8).copy()}
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows, np.r_[0, np.ones(n, np.uint8)].astype(np.uint8))
+    ix.set_graph(offs, ids)
+    ix.qg_set_quantizer(np.zeros(dim, np.float32), local[:, 1:17, :])
+    ix.qg_build_graph(codes, maxe)
+    return qg, rows, ix
+
+
+@pytest.mark.parametrize("dim", [129, 256, 512])
+def test_qg_wide_subspace_counts_exact(dim):
+    """Subspace counts past one pair per lane (M = 129: a padded odd subspace
+    and idle lanes; 256: two pairs per lane; 512: four) give the oracle's ids,
+    float distance bits and work counters -- the i8 matrix-core sum of the ADC
+    (table bytes stored as v - 128) is exact for every lane layout."""
+    qg, rows, ix = _synthetic_qg(dim, 1200, 40, 7 + dim)
+    rng = np.random.default_rng(dim)
+    qs = rng.random((6, dim), dtype=np.float32)
+    seeds = [np.array([1 + 37 * i, 600 + i], np.uint32) for i in range(len(qs))]
+    for k, eps, exp in [(10, 0.1, 3.0), (20, 0.05, 1.0)]:
+        gi, gd, gn, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_GIVEN,
+                                       seeds=seeds)
+        for qi, q in enumerate(qs):
+            oid, od, ocnt = O.qg_search(qg, rows, q, seeds[qi], k, np.float32(eps), np.float32(exp))
+            assert list(gi[qi, :gn[qi]]) == list(oid), (dim, k, qi)
+            assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32)), (dim, k, qi)
+            assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt], (dim, k, qi)
+    ix.close()
