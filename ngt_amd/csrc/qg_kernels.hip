@@ -268,6 +268,25 @@ __global__ void __launch_bounds__(256) ngt_qg_train_kernel(QgTrainArgs a) {
 // sh = 0 (low nibbles) or 4 (high nibbles).  Two v_perm_b32 look the 3 low
 // index bits up in the lower and upper 8 table bytes; a third picks, per
 // byte, lower or upper by index bit 3 (selector b or 4 + b).
+// The pick selector is one v_and_or_b32 (mask from an SGPR, base 0x03020100
+// from a VGPR: VOP3 on gfx9 takes no literal and one scalar operand), which
+// the compiler otherwise emits as v_and + v_or.
+__device__ __forceinline__ uint32_t and_or_b32(uint32_t x, uint32_t mask, uint32_t base) {
+  uint32_t r;
+  asm volatile("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask), "v"(base));
+  return r;
+}
+
+template <int SH>
+__device__ __forceinline__ uint32_t lut16(uint32_t w, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                          uint32_t base) {
+  const uint32_t sel = (w >> SH) & 0x07070707u;
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, sel);
+  const uint32_t hi = __builtin_amdgcn_perm(t3, t2, sel);
+  const uint32_t pick = and_or_b32(w >> (SH + 1), 0x04040404u, base);
+  return __builtin_amdgcn_perm(hi, lo, pick);
+}
+
 template <int SH>
 __device__ __forceinline__ uint32_t lut16(uint32_t w, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3) {
   const uint32_t sel = (w >> SH) & 0x07070707u;
@@ -340,25 +359,45 @@ __device__ __forceinline__ qg_i32x4 qg_onehot_b() {
   return b;
 }
 
+// The MFMA part for one block: returns this lane's sum of the four C
+// registers (rows 4g..4g+3 of column lane & 15, g = lane >> 4).
 template <int PPL>
-__device__ __forceinline__ uint32_t adc_sum_mfma(const LaneLut<PPL>& L, const uint4 (&c)[PPL], qg_i32x4 onehot) {
+__device__ __forceinline__ uint32_t adc_part_mfma(const LaneLut<PPL>& L, const uint4 (&c)[PPL], qg_i32x4 onehot,
+                                                  uint32_t base) {
   qg_i32x4 acc = {0, 0, 0, 0};
 #pragma unroll
   for (int s = 0; s < PPL; s++) {
     const uint32_t* t = L.t[s];
     qg_i32x4 ev, od;
-    ev[0] = (int)lut16<0>(c[s].x, t[0], t[1], t[2], t[3]);  // objects 0,2,4,6
-    ev[1] = (int)lut16<4>(c[s].x, t[0], t[1], t[2], t[3]);  // 1,3,5,7
-    ev[2] = (int)lut16<0>(c[s].y, t[0], t[1], t[2], t[3]);  // 8,...,14
-    ev[3] = (int)lut16<4>(c[s].y, t[0], t[1], t[2], t[3]);  // 9,...,15
-    od[0] = (int)lut16<0>(c[s].z, t[4], t[5], t[6], t[7]);
-    od[1] = (int)lut16<4>(c[s].z, t[4], t[5], t[6], t[7]);
-    od[2] = (int)lut16<0>(c[s].w, t[4], t[5], t[6], t[7]);
-    od[3] = (int)lut16<4>(c[s].w, t[4], t[5], t[6], t[7]);
+    ev[0] = (int)lut16<0>(c[s].x, t[0], t[1], t[2], t[3], base);  // objects 0,2,4,6
+    ev[1] = (int)lut16<4>(c[s].x, t[0], t[1], t[2], t[3], base);  // 1,3,5,7
+    ev[2] = (int)lut16<0>(c[s].y, t[0], t[1], t[2], t[3], base);  // 8,...,14
+    ev[3] = (int)lut16<4>(c[s].y, t[0], t[1], t[2], t[3], base);  // 9,...,15
+    od[0] = (int)lut16<0>(c[s].z, t[4], t[5], t[6], t[7], base);
+    od[1] = (int)lut16<4>(c[s].z, t[4], t[5], t[6], t[7], base);
+    od[2] = (int)lut16<0>(c[s].w, t[4], t[5], t[6], t[7], base);
+    od[3] = (int)lut16<4>(c[s].w, t[4], t[5], t[6], t[7], base);
     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ev, onehot, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(od, onehot, acc, 0, 0, 0);
   }
-  uint32_t r = (uint32_t)(acc[0] + acc[1]) + (uint32_t)(acc[2] + acc[3]);
+  return (uint32_t)(acc[0] + acc[1]) + (uint32_t)(acc[2] + acc[3]);
+}
+
+// Fold of four blocks' parts: lane group g (lane >> 4) ends with the signed
+// sum of block g's object lane & 15 -- one epilogue serves four blocks.
+__device__ __forceinline__ uint32_t fold4(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
+  const auto x = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);  // lanes < 32 keep p0, else p2
+  const auto y = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
+  const uint32_t a = x[0] + x[1], b = y[0] + y[1];
+  const auto z = __builtin_amdgcn_permlane16_swap(a, b, false, false);  // even rows keep a, odd rows b
+  return z[0] + z[1];
+}
+
+// Single block: every lane ends with its object lane & 15.
+template <int PPL>
+__device__ __forceinline__ uint32_t adc_sum_mfma(const LaneLut<PPL>& L, const uint4 (&c)[PPL], qg_i32x4 onehot,
+                                                 uint32_t base) {
+  uint32_t r = adc_part_mfma<PPL>(L, c, onehot, base);
   {
     const auto x = __builtin_amdgcn_permlane32_swap(r, r, false, false);  // lane ^ 32
     r = x[0] + x[1];
@@ -476,7 +515,8 @@ __device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* c
   const uint32_t nb = n == 0 ? 0 : (n - 1) / 16 + 1;
   const uint64_t blk = (uint64_t)8 * Me;
   const qg_i32x4 onehot = qg_onehot_b();
-  (void)onehot;
+  const uint32_t base = 0x03020100u;
+  (void)onehot; (void)base;
   // blocks whose loads are in flight together (bounded by VGPRs)
   constexpr int NBF = PPL >= 4 ? 1 : (PPL == 2 ? 2 : 4);
   for (uint32_t b0 = 0; b0 < nb; b0 += NBF) {
@@ -501,7 +541,7 @@ __device__ __forceinline__ void adc_node(const LaneLut<PPL>& L, const uint8_t* c
         const uint32_t o = (b0 + j) * 16 + qg_obj_of_lane(lane);
         if ((lane & 3) == 0 && o < n) dists[o] = adc_epilogue(r, scale, toff);
 #else
-        const uint32_t r = adc_sum_mfma<PPL>(L, c[j], onehot);
+        const uint32_t r = adc_sum_mfma<PPL>(L, c[j], onehot, base);
         const uint32_t o = (b0 + j) * 16 + ((uint32_t)lane & 15u);
         if (lane < 16 && o < n) dists[o] = adc_epilogue_total(r, Me, scale, toff);
 #endif
@@ -570,22 +610,36 @@ __device__ __forceinline__ uint32_t ids_and_adc(const LaneLut<PPL>& L, const uin
     }
   }
   const uint32_t nb = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+#if NGT_AMD_QG_VALU_REDUCE
 #pragma unroll
   for (int j = 0; j < NB; j++) {
     if ((uint32_t)j < nb) {
-#if NGT_AMD_QG_VALU_REDUCE
       uint32_t v[16];
       block_partials<PPL>(L, c[j], v);
       const uint32_t r = reduce_scatter16(v);
       const uint32_t o = (uint32_t)j * 16 + qg_obj_of_lane(lane);
       if ((lane & 3) == 0 && o < deg) dists[o] = adc_epilogue(r, scale, toff);
-#else
-      const uint32_t r = adc_sum_mfma<PPL>(L, c[j], onehot);
-      const uint32_t o = (uint32_t)j * 16 + ((uint32_t)lane & 15u);
-      if (lane < 16 && o < deg) dists[o] = adc_epilogue_total(r, Me, scale, toff);
-#endif
     }
   }
+#else
+  // four blocks per fold and epilogue: lane group g writes block 4q + g
+  const uint32_t base = 0x03020100u;
+#pragma unroll
+  for (int q = 0; q < (NB + 3) / 4; q++) {
+    if ((uint32_t)(4 * q) < nb) {
+      uint32_t part[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int j = 4 * q + u;
+        part[u] = 0;
+        if (j < NB && (uint32_t)j < nb) part[u] = adc_part_mfma<PPL>(L, c[j < NB ? j : 0], onehot, base);
+      }
+      const uint32_t r = fold4(part[0], part[1], part[2], part[3]);
+      const uint32_t o = (uint32_t)(4 * q) * 16 + (uint32_t)lane;
+      if (o < deg) dists[o] = adc_epilogue_total(r, Me, scale, toff);
+    }
+  }
+#endif
   seen[0] = seen[1] = 0;
 #pragma unroll
   for (int cc = 0; cc < NC; cc++)
