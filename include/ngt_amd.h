@@ -332,6 +332,53 @@ int ngt_amd_qg_search_device(ngt_amd_index *index, const ngt_amd_qg_search_param
                              const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,
                              float *d_dists, uint32_t *d_n, uint64_t *d_counters, void *stream);
 
+/* ---- NGTQ IVF-ADC ------------------------------------------------------- *
+ *   ngt_amd_ngtq_open          <- NGTQ::Index(path) (lib/NGT/NGTQ/Quantizer.h:2832-2836,
+ *                                 QuantizerInstance::open :1520-1570): prf, global/
+ *                                 (the global codebook, an NGT index), local-<i>/obj,
+ *                                 ivt and the object list obj, loaded into HBM.
+ *   ngt_amd_ngtq_set           <- the same state from host arrays; the index is
+ *                                 the global codebook (rows/graph/tree set).
+ *   ngt_amd_ngtq_search[_device] <- NGTQ::Index::search(object, objs, size,
+ *                                 expansion, aggregationMode, epsilon) (:2877-2883)
+ *                                 = QuantizerInstance::search (:2471-2549):
+ *                                 searchGlobalCodebook (:2248-2262, linear when
+ *                                 epsilon < 0 or >= FLT_MAX, the CLI's "-e -"),
+ *                                 aggregateObjects* (:2266-2441) with the float-LUT
+ *                                 ADC (:942-953), residual distances (:579-608,
+ *                                 :1102-1153) or exact distances, refineDistance.
+ * Float L2 indexes with 2-byte local ids; the cache and refine modes need a
+ * subvector dimension that is a multiple of 8 (the reference reads whole
+ * 8-float blocks). */
+#define NGT_AMD_NGTQ_APPROXIMATE 0   /* AggregationModeApproximateDistance                */
+#define NGT_AMD_NGTQ_LOOKUP_TABLE 1  /* AggregationModeApproximateDistanceWithLookupTable */
+#define NGT_AMD_NGTQ_CACHE 2         /* AggregationModeApproximateDistanceWithCache       */
+#define NGT_AMD_NGTQ_REFINE 3        /* AggregationModeExactDistanceThroughApproximateDistance */
+#define NGT_AMD_NGTQ_EXACT 4         /* AggregationModeExactDistance                      */
+typedef struct {
+  uint32_t size;         /* results per query                                      */
+  float expansion;       /* approximateSearchSize = size * expansion                */
+  float epsilon;         /* global-codebook search; < 0 => linear search (FLT_MAX)  */
+  int32_t mode;          /* NGT_AMD_NGTQ_*                                          */
+} ngt_amd_ngtq_search_params;
+
+int ngt_amd_ngtq_open(const char *path, int device, ngt_amd_index **out);
+/* local: [N][16][dsub] local centroids (ids 1..16); list_off [nlists+1] CSR of
+ * the inverted lists by global centroid id; eids [entries] object ids;
+ * elids [entries][N] uint16 local ids (0 = the object is its centroid);
+ * objects [object_records][dimension] floats (the object list, record 0 unused). */
+int ngt_amd_ngtq_set(ngt_amd_index *index, const float *local, uint32_t N, uint32_t dsub,
+                     const uint64_t *list_off, uint64_t nlists, const uint32_t *eids,
+                     const uint16_t *elids, uint64_t nentries, const float *objects,
+                     uint64_t object_records);
+/* Host pointers; ids/dists [nq][size] ascending (distance, id), n [nq]. */
+int ngt_amd_ngtq_search(ngt_amd_index *index, const ngt_amd_ngtq_search_params *params,
+                        const float *queries, uint32_t nq, uint32_t *ids, float *dists, uint32_t *n);
+/* Device pointers; queries are prepared padded float rows, query_bytes apart. */
+int ngt_amd_ngtq_search_device(ngt_amd_index *index, const ngt_amd_ngtq_search_params *params,
+                               const void *d_queries, uint64_t query_bytes, uint32_t nq,
+                               uint32_t *d_ids, float *d_dists, uint32_t *d_n, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,6 +14,10 @@ class QgSearchParams(Structure):
                 ("seed_mode", c_int32), ("visited_hash_log2", c_int32)]
 
 
+class NgtqSearchParams(Structure):
+    _fields_ = [("size", c_uint32), ("expansion", c_float), ("epsilon", c_float), ("mode", c_int32)]
+
+
 class BuildParams(Structure):
     _fields_ = [("edge_size_for_creation", c_int32), ("edge_size_for_search", c_int32),
                 ("batch_size_for_creation", c_int32), ("seed_size", c_int32), ("epsilon_for_creation", c_float),
@@ -96,6 +100,11 @@ def declare(L):
         "ngt_amd_qg_search": (c_int, [vp, POINTER(QgSearchParams), vp, c_uint32, vp, vp, vp, vp, vp, vp]),
         "ngt_amd_qg_search_device": (c_int, [vp, POINTER(QgSearchParams), vp, c_uint64, c_uint32, vp, vp, vp,
                                              vp, vp, vp, vp]),
+        "ngt_amd_ngtq_open": (c_int, [c_char_p, c_int, POINTER(vp)]),
+        "ngt_amd_ngtq_set": (c_int, [vp, vp, c_uint32, c_uint32, vp, c_uint64, vp, vp, c_uint64, vp, c_uint64]),
+        "ngt_amd_ngtq_search": (c_int, [vp, POINTER(NgtqSearchParams), vp, c_uint32, vp, vp, vp]),
+        "ngt_amd_ngtq_search_device": (c_int, [vp, POINTER(NgtqSearchParams), vp, c_uint64, c_uint32, vp, vp, vp,
+                                               vp]),
         # ---- include/NGT/Capi.h
         "ngt_open_index": (vp, [c_char_p, vp]),
         "ngt_create_graph_and_tree": (vp, [c_char_p, vp, vp]),

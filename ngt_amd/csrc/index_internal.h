@@ -72,6 +72,19 @@ struct QgState {
   bool has_graph = false;
 };
 
+// NGTQ IVF-ADC quantizer attached to a global-codebook index (ivf_api.cpp)
+struct IvfState {
+  bool ready = false;
+  uint32_t N = 0, dsub = 0, lid_stride = 0;
+  uint64_t nlists = 0, nentries = 0;
+  uint64_t object_records = 0;   // ObjectList::size() (records incl. slot 0)
+  DevBuf<float> local;           // [N][17][dsub]
+  DevBuf<uint64_t> list_off;     // [nlists + 1]
+  DevBuf<uint32_t> eids;         // [nentries]
+  DevBuf<uint16_t> elids;        // [nentries][lid_stride]
+  DevBuf<uint8_t> orows;         // [object_records][row_bytes]
+};
+
 // Scratch owned by one in-flight search launch.  One context per HIP stream
 // a caller searches on, so consecutive batches on different streams run
 // concurrently (the next batch's waves fill the CUs the previous batch's
@@ -91,6 +104,8 @@ struct SearchCtx {
   DevBuf<uint16_t> sqh, sql;     // matrix-core scan: queries in fragment order
   DevBuf<float> shb;             // matrix-core scan: per-query filter base
   DevBuf<uint64_t> gthr;         // matrix-core scan: per-query k-th key shared by the parts
+  DevBuf<uint32_t> ivf_cid, ivf_cn;  // NGTQ: global-codebook search results [nq][cbs], [nq]
+  DevBuf<float> ivf_cd;
   DevBuf<int> err;               // device error flag of the launches on this stream
   ~SearchCtx() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -220,6 +235,7 @@ struct ngt_amd_index {
   int cu_count = 256;
   size_t lds_per_cu = 160 * 1024;
   QgState qg;                      // NGTQG quantized graph (qg_api.cpp)
+  ngt_amd::IvfState ivf;           // NGTQ IVF-ADC quantizer (ivf_api.cpp)
 };
 
 namespace ngt_amd {

@@ -365,4 +365,37 @@ hipError_t launch_qg_train(const QgTrainArgs& a, hipStream_t s);
 size_t qg_search_lds_bytes(const QgSearchArgs& a);
 hipError_t launch_qg_search(const QgSearchArgs& a, uint32_t slots, hipStream_t s);
 
+// NGTQ IVF-ADC aggregation (ivf_kernels.hip): NGTQ::AggregationMode values
+// the kernel distinguishes.
+enum IvfMode : int { kIvfApprox = 0, kIvfCache = 1, kIvfLut = 2, kIvfExact = 3, kIvfRefine = 4 };
+
+struct IvfSearchArgs {
+  const uint8_t* queries;        // prepared padded float rows, query_bytes apart
+  uint64_t query_bytes;
+  uint32_t nq;
+  int dp;
+  const uint32_t* cent_ids;      // [nq][cent_stride] global-codebook search results
+  const float* cent_d;
+  const uint32_t* cent_n;        // [nq]
+  uint32_t cent_stride;
+  const uint8_t* grows;          // global centroid rows (padded floats)
+  uint64_t grow_bytes;
+  const float* local;            // [N][17][dsub] local centroids (entry 0 unused)
+  uint32_t N, dsub, lid_stride;  // lid_stride: uint16 local ids per entry
+  const uint64_t* list_off;      // [nlists + 1] inverted lists by global id
+  uint32_t nlists;
+  const uint32_t* eids;          // [entries] object ids
+  const uint16_t* elids;         // [entries][lid_stride] local ids
+  const uint8_t* orows;          // object list rows (padded floats)
+  uint64_t orow_bytes;
+  uint32_t size;                 // result size
+  uint64_t ass;                  // approximateSearchSize
+  int mode;                      // IvfMode
+  uint32_t* out_ids;             // [nq][size]
+  float* out_dists;
+  uint32_t* out_n;               // [nq]
+};
+size_t ivf_search_lds_bytes(const IvfSearchArgs& a);
+hipError_t launch_ivf_search(const IvfSearchArgs& a, hipStream_t s);
+
 }  // namespace ngt_amd

@@ -770,3 +770,160 @@ void ngto_qg_search_batch(const float *rows, size_t dp, size_t nrows, const uint
   }
   (void)nthreads;
 }
+
+/* ---------------------------------------------------------------------------
+ * NGTQ IVF-ADC (lib/NGT/NGTQ/Quantizer.h).  The per-(subspace, centroid)
+ * residual terms follow the instruction sequences of the reference's
+ * -Ofast -march=native build (objdump of createFloatL2DistanceLookup,
+ * QuantizedObjectDistanceFloat::operator()(Object&, size_t, void*[, LUT&])),
+ * pinned by tests/golden/ngtq_n{8,16,32}.
+ * ------------------------------------------------------------------------- */
+
+/* createFloatL2DistanceLookup (:683-706): float d over the subvector. */
+static float ngtq_lut_l(const float *o, const float *g, const float *l, size_t dsub) {
+  float acc = 0.0f;
+  size_t i = 0;
+  if (dsub >= 16) {
+    float a[16] = {0};
+    for (; i + 16 <= dsub; i += 16)
+      for (int j = 0; j < 16; j++) {
+        float s = o[i + j] - (g[i + j] + l[i + j]);
+        a[j] = fmaf(s, s, a[j]);
+      }
+    for (int h = 8; h >= 1; h >>= 1)
+      for (int j = 0; j < h; j++) a[j] = a[j + h] + a[j];
+    acc = a[0];
+  }
+  if (dsub - i >= 8) {
+    float b[8];
+    for (int j = 0; j < 8; j++) {
+      float s = (o[i + j] - l[i + j]) - g[i + j];
+      b[j] = s * s;
+    }
+    for (int h = 4; h >= 1; h >>= 1)
+      for (int j = 0; j < h; j++) b[j] = b[j + h] + b[j];
+    acc = acc + b[0];
+    i += 8;
+  }
+  for (; i < dsub; i++) {
+    float s = o[i] - (g[i] + l[i]);
+    acc = fmaf(s, s, acc);
+  }
+  return acc;
+}
+
+/* operator()(Object&, size_t, void*, DistanceLookupTable&) (:1102-1153): the
+ * 8-lane AVX block loop (dsub a multiple of 8). */
+static double ngtq_sub_c(const float *o, const float *g, const float *l, size_t dsub) {
+  float a[8] = {0};
+  for (size_t i = 0; i < dsub; i += 8)
+    for (int j = 0; j < 8; j++) {
+      float s = o[i + j] - (g[i + j] + l[i + j]);
+      a[j] = fmaf(s, s, a[j]);
+    }
+  float x[4];
+  for (int j = 0; j < 4; j++) x[j] = a[j] + a[j + 4];
+  return (double)((x[0] + x[1]) + (x[3] + x[2]));
+}
+
+/* getL2DistanceFloat (:579-608): the per-subspace double sum. */
+static double ngtq_sub_a(const float *o, const float *g, const float *l, size_t dsub) {
+  double d = 0.0;
+  size_t i = 0;
+  if (dsub >= 16) {
+    double a[8] = {0};
+    for (; i + 16 <= dsub; i += 16)
+      for (int j = 0; j < 8; j++) {
+        double lo = (double)(o[i + j] - (g[i + j] + l[i + j]));
+        double hi = (double)(o[i + j + 8] - (g[i + j + 8] + l[i + j + 8]));
+        a[j] = a[j] + fma(lo, lo, hi * hi);
+      }
+    for (int h = 4; h >= 1; h >>= 1)
+      for (int j = 0; j < h; j++) a[j] = a[j + h] + a[j];
+    d = a[0];
+  }
+  if (dsub - i >= 8) {
+    double t[4];
+    for (int j = 0; j < 4; j++) {
+      double lo = (double)(o[i + j] - (g[i + j] + l[i + j]));
+      double hi = (double)(o[i + j + 4] - (g[i + j + 4] + l[i + j + 4]));
+      t[j] = fma(lo, lo, hi * hi);
+    }
+    d = d + ((t[3] + t[1]) + (t[2] + t[0]));
+    i += 8;
+  }
+  for (; i < dsub; i++) {
+    double s = (double)(o[i] - (g[i] + l[i]));
+    d = fma(s, s, d);
+  }
+  return d;
+}
+
+static int od_cmp_desc(const void *pa, const void *pb) { return -od_cmp(pa, pb); }
+
+size_t ngto_ngtq_aggregate(int mode, const float *query, size_t dp, const uint32_t *cent_ids,
+                           const float *cent_d, size_t ncent, const float *grows, const float *local, size_t N,
+                           size_t dsub, const uint64_t *list_off, size_t nlists, const uint32_t *eids,
+                           const uint16_t *elids, const float *orows, size_t size, uint64_t ass,
+                           uint32_t *out_ids, float *out_d) {
+  /* the ResultSet of QuantizerInstance::search (:2508-2531): every aggregated
+   * entry, later popped into ascending order and cut to `size` */
+  size_t cap = 1024, n = 0;
+  od_t *all = (od_t *)malloc(cap * sizeof(od_t));
+  double *tab = (double *)malloc(N * 17 * sizeof(double));
+  for (size_t ci = 0; ci < ncent; ci++) {
+    uint32_t gid = cent_ids[ci];
+    if (gid >= nlists) continue; /* invertedIndex[id] == 0 (:2425-2430) */
+    uint64_t lo = list_off[gid], len = list_off[gid + 1] - lo;
+    /* limit INT_MAX while the result set is empty (:2432) */
+    uint64_t lim = n == 0 ? (uint64_t)INT_MAX : ass;
+    const float *g = grows + (size_t)gid * dp;
+    if (mode != 4)
+      for (size_t li = 0; li < N; li++)
+        for (size_t k = 1; k <= 16; k++) {
+          const float *o = query + li * dsub, *gg = g + li * dsub, *l = local + (li * 17 + k) * dsub;
+          tab[li * 17 + k] = mode == 1 ? (double)ngtq_lut_l(o, gg, l, dsub)
+                                       : (mode == 0 ? ngtq_sub_a(o, gg, l, dsub) : ngtq_sub_c(o, gg, l, dsub));
+        }
+    for (uint64_t j = 0; j < len && n < lim; j++) {
+      uint64_t e = lo + j;
+      const uint16_t *lid = elids + e * N;
+      float d;
+      if (lid[0] == 0) {
+        d = cent_d[ci]; /* the object is the centroid (:2275-2277) */
+      } else if (mode == 4) {
+        d = ngto_distance(NGTO_L2, NGTO_FLOAT, query, orows + (size_t)eids[e] * dp, dp);
+      } else {
+        double s = 0.0;
+        for (size_t li = 0; li < N; li++) s = s + tab[li * 17 + lid[li]];
+        d = (float)sqrt(s);
+      }
+      if (n == cap) {
+        cap *= 2;
+        all = (od_t *)realloc(all, cap * sizeof(od_t));
+      }
+      all[n].id = eids[e];
+      all[n].d = d;
+      n++;
+    }
+    if (n >= ass) break;
+  }
+  qsort(all, n, sizeof(od_t), od_cmp);
+  size_t m = n < size ? n : size;
+  if (mode == 3) { /* refineDistance (:2450-2460) */
+    for (size_t i = 0; i < m; i++) all[i].d = ngto_distance(NGTO_L2, NGTO_FLOAT, query, orows + (size_t)all[i].id * dp, dp);
+    qsort(all, m, sizeof(od_t), od_cmp);
+  }
+  for (size_t i = 0; i < m; i++) {
+    out_ids[i] = all[i].id;
+    out_d[i] = all[i].d;
+  }
+  free(all);
+  free(tab);
+  (void)od_cmp_desc;
+  return m;
+}
+
+double ngto_ngtq_term(int mode, const float *o, const float *g, const float *l, size_t dsub) {
+  return mode == 1 ? (double)ngtq_lut_l(o, g, l, dsub) : (mode == 0 ? ngtq_sub_a(o, g, l, dsub) : ngtq_sub_c(o, g, l, dsub));
+}

@@ -143,6 +143,24 @@ void ngto_qg_search_batch(const float *rows, size_t dp, size_t nrows, const uint
                           float result_expansion, float radius, size_t out_stride, uint32_t *out_ids,
                           float *out_dists, uint32_t *out_n, uint64_t *counters, int nthreads);
 
+/* NGTQ IVF-ADC: the aggregation of QuantizerInstance::search
+ * (lib/NGT/NGTQ/Quantizer.h:2499-2549) for one query, given the
+ * global-codebook search result (cent_ids/cent_d, ncent entries in order).
+ * mode = NGTQ::AggregationMode: 0 approximate (getL2DistanceFloat :579-608),
+ * 1 lookup table (createFloatL2DistanceLookup :683-706 + :942-953), 2 cache
+ * (:1102-1153), 3 cache + refineDistance (:2450-2460), 4 exact.  grows /
+ * orows: padded global-centroid / object-list rows (dp floats); local
+ * [N][17][dsub] (slot 0 unused); inverted lists CSR by global id with N
+ * uint16 local ids per entry.  Returns min(#aggregated, size) results in
+ * ascending (distance, id). */
+size_t ngto_ngtq_aggregate(int mode, const float *query, size_t dp, const uint32_t *cent_ids,
+                           const float *cent_d, size_t ncent, const float *grows, const float *local, size_t N,
+                           size_t dsub, const uint64_t *list_off, size_t nlists, const uint32_t *eids,
+                           const uint16_t *elids, const float *orows, size_t size, uint64_t ass,
+                           uint32_t *out_ids, float *out_d);
+/* One residual term of mode 0/1/2 (float LUT entry as double for mode 1). */
+double ngto_ngtq_term(int mode, const float *o, const float *g, const float *l, size_t dsub);
+
 #ifdef __cplusplus
 }
 #endif

@@ -268,3 +268,26 @@ def serialize_qg_grp(q):
         out.append(struct.pack("<I", b - a) + q["qids"][a:b].astype(np.uint32).tobytes())
         out.append(q["codes"][int(q["code_off"][v]):int(q["code_off"][v + 1])].tobytes())
     return b"".join(out)
+
+
+def read_array_file(path, dim, dtype=np.float32):
+    """NGTQ object list (ArrayFile<NGT::Object>, lib/NGT/ArrayFile.h:35-46,
+    136-145): {u64 recordSize, u64 reserve}, then per record a 16-byte
+    {bool deleteFlag, u64 reserve} head and recordSize bytes of the object.
+    Returns rows[n, dim] (record 0 is the unused slot)."""
+    raw = open(path, "rb").read()
+    rs = struct.unpack_from("<Q", raw, 0)[0]
+    n = (len(raw) - 16) // (16 + rs)
+    a = np.frombuffer(raw, np.uint8, n * (16 + rs), 16).reshape(n, 16 + rs)[:, 16:16 + dim * np.dtype(dtype).itemsize]
+    return a.copy().view(dtype).reshape(n, dim)
+
+
+def write_array_file(path, rows):
+    """Inverse of read_array_file (record 0 written as all zeros)."""
+    rows = np.ascontiguousarray(rows, dtype=np.float32)
+    rs = rows.shape[1] * 4
+    with open(path, "wb") as f:
+        f.write(struct.pack("<QQ", rs, 0))
+        for r in rows:
+            f.write(b"\0" * 16)
+            f.write(r.tobytes())

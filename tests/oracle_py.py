@@ -309,3 +309,90 @@ def qg_search_batch(qg, rows, queries, seeds, k, epsilon, expansion, luts, scale
                            queries.ctypes.data, nq, seeds.ctypes.data, so.ctypes.data, k, epsilon, expansion,
                            radius, stride, ids.ctypes.data, ds.ctypes.data, n.ctypes.data, cnt.ctypes.data, threads)
     return ids, ds, n, cnt
+
+
+# ---------------------------------------------------------------------------
+# NGTQ IVF-ADC (lib/NGT/NGTQ/Quantizer.h:2471-2549)
+# ---------------------------------------------------------------------------
+NGTQ_MODES = {"a": 0, "l": 1, "c": 2, "r": 3, "e": 4}
+
+
+def load_ngtq(index_dir, objects):
+    """An NGTQ index directory (ngtq create) as arrays: global codebook rows /
+    graph / tree / property, local [N, 17, dsub], inverted lists in CSR
+    (list_off by global id, eids, elids [E, N]) and the object list
+    `objects` [records, dim] (record 0 unused)."""
+    import ngt_files as F
+    prop = F.read_prf(os.path.join(index_dir, "prf"))
+    dim, N = int(prop["Dimension"]), int(prop["LocalDivisionNo"])
+    dsub = dim // N
+    G, _ = F.read_obj(os.path.join(index_dir, "global", "obj"), dim, np.float32)
+    goffs, gids, _ = F.read_grp(os.path.join(index_dir, "global", "grp"))
+    gtree = F.read_tre(os.path.join(index_dir, "global", "tre"), dim, np.float32)
+    gprop = F.read_prf(os.path.join(index_dir, "global", "prf"))
+    local = np.stack([F.read_obj(os.path.join(index_dir, "local-%d" % i, "obj"), dsub, np.float32)[0][:17, :dsub]
+                      for i in range(N)])
+    ents = F.read_ivt(os.path.join(index_dir, "ivt"))
+    nlists = min(max(ents) + 1, G.shape[0]) if ents else 1
+    list_off = np.zeros(nlists + 1, np.uint64)
+    eids, elids = [], []
+    for gid in range(nlists):
+        if gid in ents:
+            eids.append(ents[gid][0])
+            elids.append(ents[gid][1][:, :N])
+        list_off[gid + 1] = list_off[gid] + (len(ents[gid][0]) if gid in ents else 0)
+    dp = G.shape[1]
+    orows = np.zeros((objects.shape[0], dp), np.float32)
+    orows[:, :dim] = objects[:, :dim]
+    return {"dim": dim, "N": N, "dsub": dsub, "G": G, "goffs": goffs, "gids": gids, "gtree": gtree,
+            "gprop": gprop, "local": np.ascontiguousarray(local, np.float32), "list_off": list_off,
+            "eids": np.concatenate(eids).astype(np.uint32) if eids else np.zeros(0, np.uint32),
+            "elids": np.ascontiguousarray(np.concatenate(elids), np.uint16) if elids else np.zeros((0, N), np.uint16),
+            "orows": orows}
+
+
+def ngtq_search(st, query, mode, size, expansion, epsilon):
+    """NGTQ::Index::search(object, objs, size, expansion, mode, epsilon)
+    (Quantizer.h:2877-2883 -> :2471-2549); epsilon None = linear
+    global-codebook search (the CLI's '-e -')."""
+    L = lib()
+    if not getattr(L, "_ngtq", False):
+        L.ngto_ngtq_aggregate.restype = ctypes.c_size_t
+        L.ngto_ngtq_aggregate.argtypes = [ctypes.c_int] + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                          ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        L._ngtq = True
+    G = st["G"]
+    dp = G.shape[1]
+    q = np.zeros(dp, np.float32)
+    q[:len(query)] = query
+    ass = int(np.float32(size) * np.float32(expansion))
+    cbs = ass // (st["orows"].shape[0] // G.shape[0]) + 1
+    if epsilon is None:
+        cids, cds = linear_search("l2", G, q, cbs)
+    else:
+        seeds, _, _ = tree_seeds("l2", st["gtree"], q, cbs, int(st["gprop"]["SeedSize"]))
+        cids, cds, _ = search("l2", G, st["goffs"], st["gids"], q, seeds, cbs, np.float32(epsilon),
+                              edge_size=int(st["gprop"]["EdgeSizeForSearch"]))
+    cids = np.ascontiguousarray(cids, np.uint32)
+    cds = np.ascontiguousarray(cds, np.float32)
+    out_i = np.zeros(size, np.uint32)
+    out_d = np.zeros(size, np.float32)
+    c = lambda a: a.ctypes.data
+    n = L.ngto_ngtq_aggregate(NGTQ_MODES[mode], c(q), dp, c(cids), c(cds), len(cids), c(G), c(st["local"]), st["N"],
+                              st["dsub"], c(st["list_off"]), len(st["list_off"]) - 1, c(st["eids"]), c(st["elids"]),
+                              c(st["orows"]), size, ass, c(out_i), c(out_d))
+    return out_i[:n].copy(), out_d[:n].copy()
+
+
+def ngtq_term(mode, o, g, l):
+    """One residual term (ngto_ngtq_term): mode 'l' float LUT entry, 'a' / 'c'
+    per-subspace double."""
+    L = lib()
+    L.ngto_ngtq_term.restype = ctypes.c_double
+    L.ngto_ngtq_term.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    a = [np.ascontiguousarray(x, np.float32) for x in (o, g, l)]
+    return L.ngto_ngtq_term(NGTQ_MODES[mode], a[0].ctypes.data, a[1].ctypes.data, a[2].ctypes.data, len(a[0]))
