@@ -12,6 +12,7 @@
 //   ngt_sample accuracy <index> <expected accuracy>
 // Output lines: "<query> <rank> <id> <distance bits as hex>" then, per query,
 // "# <query> distances=<distanceComputationCount>".
+#include <cfloat>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -22,6 +23,7 @@
 
 #include "NGT/Index.h"
 #include "NGT/NGTQ/QuantizedGraph.h"
+#include "NGT/NGTQ/Quantizer.h"
 
 using namespace std;
 
@@ -73,6 +75,28 @@ int main(int argc, char** argv) {
     if (mode == "accuracy") {
       NGT::Index index(path);
       printf("%.9g\n", index.getEpsilonFromExpectedAccuracy(atof(argv[3])));
+      return 0;
+    }
+    if (mode == "ngtq") {
+      // the `ngtq search` flow (NGTQCommand.h:272-420): allocateObject, then
+      // NGTQ::Index::search(object, objects, size, expansion, mode, epsilon)
+      NGTQ::Index index(path);
+      auto queries = read_tsv(argv[3], 128);
+      const char m = argv[6][0];
+      NGTQ::AggregationMode am = m == 'r'   ? NGTQ::AggregationModeExactDistanceThroughApproximateDistance
+                                 : m == 'e' ? NGTQ::AggregationModeExactDistance
+                                 : m == 'l' ? NGTQ::AggregationModeApproximateDistanceWithLookupTable
+                                 : m == 'c' ? NGTQ::AggregationModeApproximateDistanceWithCache
+                                            : NGTQ::AggregationModeApproximateDistance;
+      const double epsilon = string(argv[7]) == "-" ? FLT_MAX : atof(argv[7]);
+      for (size_t qi = 0; qi < queries.size(); qi++) {
+        std::vector<double> q(queries[qi].begin(), queries[qi].end());
+        NGT::Object* query = index.allocateObject(q);
+        NGT::ObjectDistances objects;
+        index.search(query, objects, atoi(argv[4]), (float)atof(argv[5]), am, epsilon);
+        print(qi, objects);
+        index.deleteObject(query);
+      }
       return 0;
     }
     if (mode == "qg") {

@@ -176,3 +176,27 @@ def test_cxx_ngtqg_matches_reference(sample):
             n = int(z["n_" + key][i])
             assert list(ids[i, :n]) == list(z["ids_" + key][i][:n]), (key, i)
             assert np.array_equal(ds[i, :n].view(np.uint32), z["dist_" + key][i][:n].view(np.uint32)), (key, i)
+
+
+@pytest.mark.gpu
+def test_cxx_ngtq_search_matches_reference(sample):
+    """NGTQ::Index(path) + search(object, objs, size, expansion, mode, epsilon)
+    through include/NGT/NGTQ/Quantizer.h reproduce the reference's
+    NGTQ::Index::search (tests/golden/ngtq_n16, make_ngtq_goldens.py)."""
+    exe, qf, d = sample
+    idx = str(d / "ngtq_n16")
+    shutil.copytree(os.path.join(GOLD, "ngtq_n16"), idx)
+    rows, _ = F.read_obj(os.path.join(GOLD, "c1_anng", "obj"), 128, np.float32)
+    F.write_array_file(os.path.join(idx, "obj"), rows[:, :128])
+    z = np.load(os.path.join(GOLD, "ngtq_n16", "goldens.npz"))
+    qtsv = str(d / "ngtq_q.tsv")
+    with open(qtsv, "w") as f:
+        for r in z["queries"]:
+            f.write("\t".join("%.9g" % x for x in r) + "\n")
+    for m, size, exp, eps, key in [("l", 10, 4, "0.1", "l_10_4_0p1"), ("r", 20, 8, "0.05", "r_20_8_0p05"),
+                                   ("c", 10, 16, "-", "c_10_16_m1")]:
+        ids, ds, _, _ = parse(run(exe, "ngtq", idx, qtsv, size, exp, m, eps), len(z["queries"]), size)
+        for i in range(len(z["queries"])):
+            n = int(z["n_" + key][i])
+            assert list(ids[i, :n]) == list(z["ids_" + key][i, :n]), (key, i)
+            assert np.array_equal(ds[i, :n].view(np.uint32), z["d_" + key][i, :n].view(np.uint32)), (key, i)
