@@ -234,6 +234,7 @@ struct ngt_amd_index {
   }
   int cu_count = 256;
   size_t lds_per_cu = 160 * 1024;
+  size_t lds_per_block = 64 * 1024;  // hipDeviceProp_t::sharedMemPerBlock
   QgState qg;                      // NGTQG quantized graph (qg_api.cpp)
   ngt_amd::IvfState ivf;           // NGTQ IVF-ADC quantizer (ivf_api.cpp)
 };

@@ -74,6 +74,7 @@ extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distanc
   ix->row_bytes = (uint64_t)ix->dp * ix->esize;
   ix->cu_count = prop.multiProcessorCount;
   ix->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
+  ix->lds_per_block = prop.sharedMemPerBlock ? prop.sharedMemPerBlock : 64 * 1024;
   if (hipStreamCreateWithFlags(&ix->stream, hipStreamDefault) != hipSuccess) {
     delete ix;
     return fail("ngt_amd_index_create: stream/event creation failed");
@@ -414,6 +415,17 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       a.cq_cap = 1024;
       a.vf_log2 = 0;
     }
+    // up to one wave per CU (a construction batch of 200): each query may take
+    // most of its CU's LDS, so the slowest searches -- which decide the batch
+    // time -- keep their visited set and unchecked keys out of HBM (a pop
+    // otherwise rescans the HBM spill: the tail of 1M ANNG construction)
+    if (nq <= (uint32_t)ix->cu_count && ix->lds_per_block >= 128 * 1024) {
+      SearchArgs b = a;
+      b.ht_log2 = 14;
+      b.cq_cap = 8192;
+      b.vf_log2 = 15;
+      if (search_lds_bytes(b, ix->otype) <= ix->lds_per_block) a = b;
+    }
   }
   if (prm->visited_hash_log2 < 0) {
     // HBM-epoch visited set (searches visiting ~1e5 ids, the C2 bench): a
@@ -459,7 +471,8 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     a.seed_off = d_seed_off;
   }
   const size_t lds = search_lds_bytes(a, ix->otype);
-  if (lds > 64 * 1024) return fail("search: k=%u needs %zu bytes of LDS per query (max 65536)", a.k, lds);
+  const size_t lds_max = std::max<size_t>(64 * 1024, std::min<size_t>(ix->lds_per_block, ix->lds_per_cu));
+  if (lds > lds_max) return fail("search: k=%u needs %zu bytes of LDS per query (max %zu)", a.k, lds, lds_max);
   if (ensure_vis_scratch(ix, c, lds, nq, s)) return -1;
   a.vis = c->vis.p;
   a.vis_stride = c->vis_stride;

@@ -163,6 +163,17 @@ __device__ __forceinline__ void eval_any(const T* qlds, const SearchArgs& a, flo
   }
 }
 
+// Chunk minima of the unchecked array: cmin[c] = the smallest key of
+// cq[64c, 64c + 64) (~0 when the chunk is empty), so a pop reads one minimum
+// per chunk and one chunk instead of every key -- the long searches of a
+// construction batch keep thousands of unchecked keys, and their pops were
+// most of the batch time.
+__device__ __forceinline__ void cq_chunk_min(const uint64_t* cq, uint64_t* cmin, uint32_t ncq, uint32_t c) {
+  const uint32_t i = 64 * c + (uint32_t)lane_id();
+  const uint64_t m = wave_min_u64(i < ncq ? cq[i] : ~0ull);
+  if (lane_id() == 0) cmin[c] = m;
+}
+
 template <int M, typename T, int NCH, int G>
 __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -178,6 +189,8 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   p += (size_t)4 * vf_words;
   st.cq = reinterpret_cast<uint64_t*>(p);
   p += (size_t)8 * a.cq_cap;
+  uint64_t* cmin = reinterpret_cast<uint64_t*>(p);
+  p += ((size_t)8 * ((a.cq_cap + 63) / 64) + 15) & ~(size_t)15;
   st.res = reinterpret_cast<uint64_t*>(p);
   p += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   st.nid = reinterpret_cast<uint32_t*>(p);
@@ -250,12 +263,14 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         const float d = st.nd[j];
         if (d <= a.radius) res_insert(st.res, nres, k, make_key(d, st.nid[j]));
       }
+      const uint32_t ncq0 = ncq;
       if (ncq + m <= a.cq_cap) {
         ncq += m;
       } else {
         nspill += ncq + m - a.cq_cap;
         ncq = a.cq_cap;
       }
+      for (uint32_t c = ncq0 >> 6; c < ((ncq + 63) >> 6); c++) cq_chunk_min(st.cq, cmin, ncq, c);
       ndist += m;
       nvisited += m;
       __syncthreads();
@@ -272,11 +287,14 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     for (;;) {
       NGT_MARK(t_rest);
       // pop the minimum key
+      // best chunk minimum (<= 128 chunks: two per lane), then the spill
       uint64_t best = ~0ull;
       uint32_t bidx = 0xffffffffu;
-      for (uint32_t i = lane; i < ncq; i += 64) {
-        const uint64_t key = st.cq[i];
-        if (key < best) { best = key; bidx = i; }
+      const uint32_t nch = (ncq + 63) >> 6;
+      if ((uint32_t)lane < nch) { best = cmin[lane]; bidx = (uint32_t)lane; }
+      if ((uint32_t)lane + 64 < nch) {
+        const uint64_t v = cmin[lane + 64];
+        if (v < best) { best = v; bidx = (uint32_t)lane + 64; }
       }
       for (uint32_t i = lane; i < nspill; i += 64) {
         const uint64_t key = spill[i];
@@ -288,12 +306,31 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       const uint64_t owner = ballot64(best == wbest);
       const int olane = __ffsll((long long)owner) - 1;
       bidx = __shfl(bidx, olane, 64);
+      if (!(bidx & 0x80000000u)) {
+        // the key's slot inside its chunk (keys are distinct)
+        const uint32_t i = 64 * bidx + (uint32_t)lane;
+        const uint64_t in = ballot64(i < ncq && st.cq[i] == wbest);
+        if (in == 0) {  // stale chunk minimum: never expected; stop this query loudly
+          if (lane == 0) atomicOr(a.error, 4);
+          break;
+        }
+        bidx = 64 * bidx + (uint32_t)(__ffsll((long long)in) - 1);
+      }
       if (lane == 0) {
         if (bidx & 0x80000000u) spill[bidx & 0x7fffffffu] = spill[nspill - 1];
         else st.cq[bidx] = st.cq[ncq - 1];
       }
-      if (bidx & 0x80000000u) nspill--; else ncq--;
-      __syncthreads();
+      if (bidx & 0x80000000u) {
+        nspill--;
+        __syncthreads();
+      } else {
+        ncq--;
+        __syncthreads();
+        // the popped slot's chunk took the last key; the last chunk lost it
+        cq_chunk_min(st.cq, cmin, ncq, bidx >> 6);
+        if ((ncq >> 6) != (bidx >> 6)) cq_chunk_min(st.cq, cmin, ncq, ncq >> 6);
+        __syncthreads();
+      }
       nexp++;
       NGT_MARK(t_pop);
 
@@ -343,9 +380,15 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
             if (ncq >= a.cq_cap) {
               ncq = compact(st.cq, ncq, expr);
               if (nspill) nspill = compact(spill, nspill, expr);
+              for (uint32_t c = 0; c < ((ncq + 63) >> 6); c++) cq_chunk_min(st.cq, cmin, ncq, c);
+              __builtin_amdgcn_wave_barrier();
             }
             if (ncq < a.cq_cap) {
-              if (lane == 0) st.cq[ncq] = key;
+              if (lane == 0) {
+                st.cq[ncq] = key;
+                const uint32_t c = ncq >> 6;
+                cmin[c] = (ncq & 63) == 0 ? key : (key < cmin[c] ? key : cmin[c]);
+              }
               ncq++;
             } else {
               if (nspill >= a.spill_cap) {
@@ -630,6 +673,7 @@ hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipSt
 
 size_t search_lds_bytes(const SearchArgs& a, int otype) {
   size_t b = (a.ht_log2 ? ((size_t)4 << a.ht_log2) : 0) + (size_t)8 * a.cq_cap;
+  b += ((size_t)8 * ((a.cq_cap + 63) / 64) + 15) & ~(size_t)15;  // chunk minima
   b += a.vf_log2 ? ((size_t)1 << a.vf_log2) / 8 : 0;
   b += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   b += 512;
