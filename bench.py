@@ -405,6 +405,7 @@ def main():
         run(chosen)
         torch.cuda.synchronize()
         kms.append(ix.last_search_kernel_ms())
+    filtered = (not qgm) and ix.last_search_filtered()
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -439,12 +440,20 @@ def main():
         me = (D + 1) // 2 * 2
         alg_bytes = c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4 + NQ * (dp * 4 + K * 8)
         kname = "ngt_qg_search_kernel"
+    elif filtered:
+        # the filtered kernel's own minimum: every distinct neighbour's 1-byte
+        # filter row, the f32 row of the seeds and of every neighbour the bound
+        # could not reject, adjacency, query, results:
+        # B(q) = (U(q) - S(q))*Dp + (S(q) + X(q))*Dp*4 + E(q)*4 + Dp*4 + k*8
+        alg_bytes = ((c[:, 0] - c[:, 7]).sum() * dp + (c[:, 7] + c[:, 6]).sum() * dp * 4 + c[:, 4].sum() * 4
+                     + NQ * (dp * 4 + K * 8))
+        kname = "ngt_graph_search_kernel"
     else:
         # B(q) = U(q)*Dp*4 + E(q)*4 + Dp*4 + k*8   
         alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + NQ * (dp * 4 + K * 8)
         kname = "ngt_graph_search_kernel"
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic, tentry = measured_traffic(args.mode, args.config, graph, chosen, args.visited)
+    traffic, tentry = measured_traffic(args.mode, args.config, graph, chosen, args.visited, filtered)
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
         tot = c[:, [5, 6, 7, 3]].mean(0)
         log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
@@ -509,6 +518,8 @@ def main():
                                        {-2: "hbm-epochs+lds-filter, accepted ids only",
                                         -1: "hbm-epochs+lds-filter"}.get(args.visited, "lds-hash")),
                        "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world),
+                       "distance_filter": ("1-byte filter copy (lower bound rejects neighbours outside the "
+                                           "exploration radius; exact f32 rows for the rest)" if filtered else "none"),
                        "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
@@ -534,6 +545,8 @@ def main():
             line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
         else:
             line["config"]["edges_read_per_query"] = float(c[:, 4].mean())
+            if filtered:
+                line["config"]["exact_neighbour_distances_per_query"] = float(c[:, 6].mean())
             if evals_per_query is not None:
                 line["config"]["evaluations_per_query"] = evals_per_query
         print(json.dumps(line), file=result_out, flush=True)
@@ -541,7 +554,7 @@ def main():
         dist.destroy_process_group()
 
 
-def measured_traffic(mode, config, graph, eps, visited):
+def measured_traffic(mode, config, graph, eps, visited, filtered=False):
     """HBM bytes per launch of the search kernel from the committed PMC passes
     (profiles/traffic.json, written from rocprofv3 FETCH_SIZE/WRITE_SIZE) for this
     exact workload and epsilon; NGT_BENCH_TRAFFIC_BYTES overrides; else None."""
@@ -555,7 +568,8 @@ def measured_traffic(mode, config, graph, eps, visited):
         return None, {}
     for e in entries:
         if (e.get("mode", "exact") == mode and e.get("config", "c2") == config and e["graph"] == graph
-                and e.get("visited", -1) == visited and abs(e["epsilon"] - eps) < 1e-7):
+                and e.get("visited", -1) == visited and abs(e["epsilon"] - eps) < 1e-7
+                and bool(e.get("filtered", False)) == bool(filtered)):
             return float(e["traffic_bytes"]), e
     return None, {}
 

@@ -82,13 +82,16 @@ typedef struct {
                                 probes; rejected neighbours met again are
                                 re-evaluated, so counters[0] counts evaluations,
                                 not the reference's distinct distance count    */
-  int32_t reserved;
+  int32_t distance_filter; /* 1-byte filter copy of L2 float rows (96/128 elements):
+                                0 = auto (launches of >= 2 queries per CU), 1 = on,
+                                -1 = off; identical results either way          */
 } ngt_amd_search_params;
 
 /* Per-query counters written by the search (8 x uint64 per query):
  * [0] distance computations (seeds + evaluated neighbours), [1] evaluated
  * neighbours (visitCount), [2] expanded nodes, [3] 1 if the visited set spilled
- * from LDS to the HBM bitmap, [4] adjacency entries read, [5..7] reserved. */
+ * from LDS to the HBM bitmap, [4] adjacency entries read, [5] largest unchecked
+ * set, [6] exact distances of neighbours, [7] seed distances. */
 #define NGT_AMD_COUNTERS_PER_QUERY 8
 
 const char *ngt_amd_last_error(void);
@@ -168,6 +171,11 @@ int ngt_amd_prepare_queries_device(ngt_amd_index *index, const float *d_in, uint
 
 /* Timing of the last search call's kernels (HIP events on the search stream), ms. */
 float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
+/* 1 if the last graph-search launch read the 1-byte filter copy of the rows
+ * (L2 float rows of 96/128 elements, launches of >= 2 queries per CU): its
+ * counters [6] are then the exact distances of neighbours the filter bound
+ * could not place outside the exploration radius, [7] the seed distances. */
+int ngt_amd_last_search_filtered(const ngt_amd_index *index);
 /* Workgroups (resident one-wave query slots) of the last search launch: per-CU
  * occupancy x CUs for a full batch, bounded by the visited-scratch HBM budget. */
 uint32_t ngt_amd_last_search_slots(const ngt_amd_index *index);

@@ -6,7 +6,7 @@ from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_i
 class SearchParams(Structure):
     _fields_ = [("k", c_uint32), ("epsilon", c_float), ("radius", c_float), ("edge_size", c_int64),
                 ("seed_mode", c_int32), ("all_leaf_nodes", c_int32),
-                ("visited_hash_log2", c_int32), ("reserved", c_int32)]
+                ("visited_hash_log2", c_int32), ("distance_filter", c_int32)]
 
 
 class QgSearchParams(Structure):
@@ -74,6 +74,7 @@ def declare(L):
         "ngt_amd_srand": (None, [c_uint]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
         "ngt_amd_last_search_slots": (c_uint32, [vp]),
+        "ngt_amd_last_search_filtered": (c_int, [vp]),
         "ngt_amd_build_begin": (c_int, [vp, POINTER(BuildParams)]),
         "ngt_amd_build_insert": (c_int, [vp, c_uint64, c_uint64]),
         "ngt_amd_build_graph_size": (c_int, [vp, u64p, u64p]),

@@ -96,6 +96,7 @@ struct SearchCtx {
   DevBuf<uint8_t> vis;           // [slots][vis_stride] visited epochs
   uint32_t slots = 0;
   uint32_t launch_slots = 0;     // workgroups (resident waves) of the last launch
+  bool launch_filtered = false;  // the last graph-search launch read the filter copy
   uint64_t vis_stride = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the search kernel
   DevBuf<uint8_t> lut;           // NGTQG: [nq][Me*16]
@@ -197,6 +198,12 @@ struct ngt_amd_index {
     uint64_t version = ~0ull;
     int passes = 0;
   } scan;
+  struct {                       // 1-byte filter copy of L2 float rows (filter_kernels.hip)
+    DevBuf<uint8_t> codes;
+    DevBuf<uint32_t> st;
+    DevBuf<float> params;        // {a, b, E, X, valid}
+    uint64_t version = ~0ull;
+  } filt;
   std::vector<uint8_t> h_valid;
   std::vector<uint64_t> h_degree_nonzero;  // for isEmpty in getRandomSeeds
   DevBuf<uint64_t> edge_off;

@@ -368,6 +368,21 @@ int ngt_amd::run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queri
   return 0;
 }
 
+// The filter copy of the current rows, built once per version of the rows
+// (synchronously: every stream's launches may read it afterwards).
+static int ensure_filter(ngt_amd_index* ix) {
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (ix->filt.version == ix->rows_version) return 0;
+  HIP_OK(ix->filt.codes.alloc((size_t)ix->nrows * ix->dp));
+  HIP_OK(ix->filt.st.alloc(8));
+  HIP_OK(ix->filt.params.alloc(8));
+  HIP_OK(launch_filter_build(ix->rows.p, ix->row_bytes, ix->nrows, ix->dp, ix->filt.codes.p, ix->filt.st.p,
+                             ix->filt.params.p, ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  ix->filt.version = ix->rows_version;
+  return 0;
+}
+
 static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_params* prm, const void* d_queries,
                       uint64_t query_bytes, uint32_t nq, const uint32_t* d_seeds,
                       const uint64_t* d_seed_off, uint32_t* d_ids, float* d_dists, uint32_t* d_n,
@@ -459,6 +474,28 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   a.out_n = d_n;
   a.counters = d_counters;
   a.error = c->err.p;
+  // 1-byte filter copy for throughput launches over L2 float rows of 96/128
+  // elements: a neighbour the bound places outside the exploration radius
+  // costs Dp bytes instead of 4 Dp (filter_kernels.hip); latency-bound small
+  // launches (construction batches) skip it, since a surviving neighbour then
+  // costs a second round trip.  NGT_AMD_FILTER=0/1 forces it off/on.
+  {
+    static const int force = [] {
+      const char* v = getenv("NGT_AMD_FILTER");
+      return v ? atoi(v) : -1;
+    }();
+    const bool shape = ix->metric == NGT_AMD_DISTANCE_L2 && ix->otype == NGT_AMD_OBJECT_FLOAT &&
+                       (ix->dp == 128 || ix->dp == 96);
+    const bool want = force >= 0 ? force != 0
+                                 : (prm->distance_filter != 0 ? prm->distance_filter > 0
+                                                              : nq >= 2u * (uint32_t)ix->cu_count);
+    if (shape && want) {
+      if (ensure_filter(ix)) return -1;
+      a.fcodes = ix->filt.codes.p;
+      a.fparams = ix->filt.params.p;
+    }
+    c->launch_filtered = a.fcodes != nullptr;
+  }
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
     if (run_tree_seeds(ix, c, d_queries, query_bytes, nq, prm->k, prm->all_leaf_nodes, s)) return -1;
@@ -562,6 +599,12 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
   }
   return run_search(ix, c, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, d_ids, d_dists,
                     d_n, d_counters, s);
+}
+
+extern "C" int ngt_amd_last_search_filtered(const ngt_amd_index* ix) {
+  if (!ix) return 0;
+  SearchCtx* c = ix->last_ctx.load();
+  return c && c->launch_filtered ? 1 : 0;
 }
 
 extern "C" uint32_t ngt_amd_last_search_slots(const ngt_amd_index* ix) {

@@ -113,6 +113,22 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   }
   return v;
 }
+__device__ __forceinline__ float wave_sum_f32(float f) {
+  uint32_t v = __float_as_uint(f);
+  v = __float_as_uint(__uint_as_float(v) + __uint_as_float(dpp_u32<0xb1>(v)));
+  v = __float_as_uint(__uint_as_float(v) + __uint_as_float(dpp_u32<0x4e>(v)));
+  v = __float_as_uint(__uint_as_float(v) + __uint_as_float(dpp_u32<0x124>(v)));
+  v = __float_as_uint(__uint_as_float(v) + __uint_as_float(dpp_u32<0x128>(v)));
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = __float_as_uint(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = __float_as_uint(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+  }
+  return __uint_as_float(v);
+}
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
   // number of set bits in mask below this lane

@@ -342,4 +342,65 @@ __device__ __forceinline__ void eval_stream(const float* qlds, const uint8_t* ro
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Lower bounds from the 1-byte filter copy (filter_kernels.hip): out[r] = the
+// float evaluation of ||q' - b c(r)|| with q' = q - a staged in LDS, i.e. of
+// ||q - x~||; the caller rejects a neighbour when this minus the error margin
+// exceeds the exploration radius.  Quad per row: lane g of a quad takes
+// elements [g E, g E + E), E = dp / 4; up to 64 rows' codes (4 x 16 rows) are
+// in flight before the first FMA.  Not bit-matched to anything: a bound.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float quad_sum(float s) {
+  s += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0xb1, 0xf, 0xf, false));  // lane ^ 1
+  s += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x4e, 0xf, 0xf, false));  // lane ^ 2
+  return s;
+}
+
+template <int NCH>
+__device__ __forceinline__ void filter_l2u8(const float* qa, const uint8_t* codes, float b, const uint32_t* ids,
+                                            float* out, int m) {
+  static_assert((NCH & 1) == 0, "whole 8-byte code words per lane");
+  constexpr int E = 4 * NCH;   // elements per lane
+  constexpr int NW = E / 8;    // 8-byte code words per lane
+  const int lane = lane_id();
+  const int g = lane & 3, rs = lane >> 2;
+  const float* q = qa + g * E;
+  for (int r0 = 0; r0 < m; r0 += 64) {
+    uint2 c[4][NW];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int r = r0 + 16 * j + rs;
+      const uint32_t id = r < m ? ids[r] : 0u;
+      const uint2* p = reinterpret_cast<const uint2*>(codes + (uint64_t)id * (4 * E)) + g * NW;
+#pragma unroll
+      for (int w = 0; w < NW; w++) c[j][w] = (j == 0 || r0 + 16 * j < m) ? p[w] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (j == 0 || r0 + 16 * j < m) {
+        float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+          const uint32_t lo = c[j][w].x, hi = c[j][w].y;
+          const float4 q0 = *reinterpret_cast<const float4*>(q + 8 * w);
+          const float4 q1 = *reinterpret_cast<const float4*>(q + 8 * w + 4);
+          float d;
+          d = __builtin_fmaf(-b, (float)(lo & 0xffu), q0.x); acc0 = __builtin_fmaf(d, d, acc0);
+          d = __builtin_fmaf(-b, (float)((lo >> 8) & 0xffu), q0.y); acc1 = __builtin_fmaf(d, d, acc1);
+          d = __builtin_fmaf(-b, (float)((lo >> 16) & 0xffu), q0.z); acc0 = __builtin_fmaf(d, d, acc0);
+          d = __builtin_fmaf(-b, (float)(lo >> 24), q0.w); acc1 = __builtin_fmaf(d, d, acc1);
+          d = __builtin_fmaf(-b, (float)(hi & 0xffu), q1.x); acc0 = __builtin_fmaf(d, d, acc0);
+          d = __builtin_fmaf(-b, (float)((hi >> 8) & 0xffu), q1.y); acc1 = __builtin_fmaf(d, d, acc1);
+          d = __builtin_fmaf(-b, (float)((hi >> 16) & 0xffu), q1.z); acc0 = __builtin_fmaf(d, d, acc0);
+          d = __builtin_fmaf(-b, (float)(hi >> 24), q1.w); acc1 = __builtin_fmaf(d, d, acc1);
+        }
+        const float s = quad_sum(acc0 + acc1);
+        const int r = r0 + 16 * j + rs;
+        if (g == 0 && r < m) out[r] = sqrtf(s);
+      }
+    }
+  }
+}
+
 }  // namespace ngt_amd

@@ -198,6 +198,22 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   st.nd = reinterpret_cast<float*>(p);
   p += 256;
   T* qlds = reinterpret_cast<T*>(p);
+  p += ((size_t)a.dp * sizeof(T) + 15) & ~(size_t)15;
+  // 1-byte filter copy (filter_kernels.hip): L2 float rows of dp = 16 * NCH
+  constexpr bool kFilterable = NCH > 0 && (NCH & 1) == 0 && M == kL2 && sizeof(T) == 4;
+  float* qa = reinterpret_cast<float*>(p);  // q - a, when filtering
+  bool use_filter = false;
+  float fa = 0.f, fb = 0.f, fe = 0.f, fx = 0.f;
+  if constexpr (kFilterable) {
+    if (a.fcodes != nullptr && a.fparams[4] != 0.0f) {
+      use_filter = true;
+      fa = a.fparams[0];
+      fb = a.fparams[1];
+      fe = a.fparams[2];
+      fx = a.fparams[3];
+    }
+  }
+  (void)qa; (void)fa; (void)fb; (void)fe; (void)fx;
 
   const uint32_t slot = blockIdx.x;
   uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
@@ -227,12 +243,28 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     float qfold = 0.f;
     if constexpr (NCH < 0 && (M == kCosine || M == kAngle))
       qfold = query_sq_fold(reinterpret_cast<const float*>(qlds), a.dp);
+    // filter margin: E plus the float evaluation error of ||q - x~||
+    double fmarg = 0.0;
+    if constexpr (kFilterable) {
+      if (use_filter) {
+        const float* qf = reinterpret_cast<const float*>(qlds);
+        float sq = 0.f;
+        for (int i = lane; i < a.dp; i += 64) {
+          qa[i] = qf[i] - fa;
+          sq = __builtin_fmaf(qf[i], qf[i], sq);
+        }
+        sq = wave_sum_f32(sq);
+        const double qn = sqrt((double)sq) * (1.0 + 1e-5);
+        fmarg = (double)fe + 0x1p-16 * (qn + (double)fx + sqrt((double)a.dp) * fabs((double)fa) + 1.0);
+        __syncthreads();
+      }
+    }
 
     bool bitmap_mode = !use_hash;
     const bool lazy = a.accepted_only && !use_hash && st.vf;
     uint32_t nvisited = 0;
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
-    uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0;
+    uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0, nexact = 0;
     uint64_t t_pop = 0, t_adj = 0, t_eval = 0, t_last = 0, t_rest = 0;
     (void)t_pop; (void)t_adj; (void)t_eval; (void)t_last; (void)t_rest;
 #ifdef NGT_AMD_STAMPS
@@ -361,15 +393,34 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         nvisited += m;
         __syncthreads();
         NGT_MARK(t_adj);
-        if (m != 0) {
-          eval_any<M, T, NCH, G>(qlds, a, qfold, st.nid, st.nd, (int)m);
+        // ids whose exact distance is needed: all fresh ones, or the ones the
+        // filter bound cannot place outside the exploration radius (kept in
+        // neighbour order)
+        uint32_t me = m;
+        if constexpr (kFilterable) {
+          if (use_filter && m != 0) {
+            filter_l2u8<NCH>(qa, a.fcodes, fb, st.nid, st.nd, (int)m);
+            __syncthreads();
+            const double fthr = (double)expr * (1.0 + 0x1p-15) + fmarg;
+            const bool keep = (uint32_t)lane < m && !((double)st.nd[lane] > fthr);
+            const uint32_t myid = (uint32_t)lane < m ? st.nid[lane] : 0u;
+            const uint64_t km = ballot64(keep);
+            __syncthreads();
+            if (keep) st.nid[mbcnt(km)] = myid;
+            me = (uint32_t)__popcll(km);
+            __syncthreads();
+          }
+        }
+        ndist += m;
+        nvisit += m;
+        nexact += me;
+        if (me != 0) {
+          eval_any<M, T, NCH, G>(qlds, a, qfold, st.nid, st.nd, (int)me);
           __syncthreads();
           NGT_MARK(t_eval);
-          ndist += m;
-          nvisit += m;
           // accept in neighbour order (Graph.cpp:471-483); only candidates
           // within the radius at batch start can be accepted.
-          uint64_t okmask = ballot64((uint32_t)lane < m && st.nd[lane] <= expr);
+          uint64_t okmask = ballot64((uint32_t)lane < me && st.nd[lane] <= expr);
           while (okmask) {
             const int j = __ffsll((long long)okmask) - 1;
             okmask &= okmask - 1;
@@ -441,8 +492,8 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         c[3] = t_rest;  // accept + loop overhead
 #else
         c[5] = maxq;
-        c[6] = 0;
-        c[7] = 0;
+        c[6] = use_filter ? nexact : ndist - (ns < ndist ? ns : ndist);  // exact distances of neighbours
+        c[7] = ns;                                                        // seed distances
 #endif
       }
     }
@@ -678,6 +729,7 @@ size_t search_lds_bytes(const SearchArgs& a, int otype) {
   b += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   b += 512;
   b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
+  if (a.fcodes) b += (size_t)a.dp * 4;  // q - a for the filter
   return b;
 }
 

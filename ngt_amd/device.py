@@ -98,11 +98,11 @@ class DeviceIndex(object):
 
     # ---- hot path -----------------------------------------------------------
     def search(self, queries, k=10, epsilon=0.1, radius=-1.0, edge_size=-1, seed_mode=SEED_TREE,
-               seeds=None, counters=True, visited_hash_log2=0):
+               seeds=None, counters=True, visited_hash_log2=0, distance_filter=0):
         """queries: [nq, dim] float.  seeds: list of arrays for SEED_GIVEN."""
         q = np.ascontiguousarray(queries, dtype=np.float32)
         nq = q.shape[0]
-        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, visited_hash_log2, 0)
+        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, visited_hash_log2, distance_filter)
         ids = np.zeros((nq, k), np.uint32)
         ds = np.zeros((nq, k), np.float32)
         n = np.zeros(nq, np.uint32)
@@ -119,13 +119,18 @@ class DeviceIndex(object):
 
     def search_device(self, d_queries, query_bytes, nq, d_ids, d_dists, d_n, d_counters=None, k=10,
                       epsilon=0.1, radius=-1.0, edge_size=-1, seed_mode=SEED_TREE, d_seeds=None,
-                      d_seed_off=None, stream=None, visited_hash_log2=0):
-        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, visited_hash_log2, 0)
+                      d_seed_off=None, stream=None, visited_hash_log2=0, distance_filter=0):
+        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, visited_hash_log2, distance_filter)
         _chk(self.L.ngt_amd_search_device(self.h, byref(prm), d_queries, query_bytes, nq, d_seeds, d_seed_off,
                                           d_ids, d_dists, d_n, d_counters, stream))
 
     def last_search_kernel_ms(self):
         return float(self.L.ngt_amd_last_search_kernel_ms(self.h))
+
+    def last_search_filtered(self):
+        """True if the last graph search read the 1-byte filter copy (counters
+        [6]: exact neighbour distances, [7]: seed distances)."""
+        return bool(self.L.ngt_amd_last_search_filtered(self.h))
 
     def last_search_slots(self):
         """Workgroups (resident query slots) of the last search launch."""

@@ -109,3 +109,64 @@ def test_visited_scratch_full_occupancy_at_shard_size():
     ix.close()
     del rows
     torch.cuda.empty_cache()
+
+
+def _search(torch, ix, qry, d_seeds, d_soff, NQ, K, eps, vis, filt):
+    dev = qry.device
+    oi = torch.zeros((NQ, K), dtype=torch.int32, device=dev)
+    od = torch.zeros((NQ, K), dtype=torch.float32, device=dev)
+    on = torch.zeros((NQ,), dtype=torch.int32, device=dev)
+    cnt = torch.zeros((NQ, 8), dtype=torch.int64, device=dev)
+    ix.search_device(qry.data_ptr(), qry.shape[1] * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(), cnt.data_ptr(),
+                     k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                     d_seed_off=d_soff.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream,
+                     visited_hash_log2=vis, distance_filter=filt)
+    torch.cuda.synchronize()
+    return (oi.cpu().numpy().view(np.uint32), od.cpu().numpy().view(np.uint32), on.cpu().numpy(), cnt.cpu().numpy(),
+            ix.last_search_filtered())
+
+
+@pytest.mark.parametrize("data", ["uniform", "sift_like", "nonfinite"])
+def test_distance_filter_identical(data):
+    """The 1-byte filter copy only rejects neighbours whose reference distance
+    is provably outside the exploration radius: ids, distance bits, result
+    counts and every reference counter (distances, visits, expansions, edges,
+    largest unchecked set) equal the unfiltered search for several epsilons
+    and visited-set modes -- on U[0,1) rows, on SIFT-like integer rows with a
+    negative offset (a != 0, coarse grid), and with a non-finite row (the
+    filter then disables itself)."""
+    import torch
+    import bench
+    dev = torch.device("cuda:0")
+    N, D, NQ, K = 60_000, 128, 1024, 10
+    x = bench.splitmix_uniform(N + NQ, D, bench.BASE_SEED + 7)
+    if data != "uniform":
+        x = np.floor(x * 256.0).astype(np.float32) - 37.0
+    rows = torch.zeros((N + 1, D), dtype=torch.float32, device=dev)
+    rows[1:] = torch.from_numpy(x[:N]).to(dev)
+    if data == "nonfinite":
+        rows[N // 2, 3] = float("inf")
+    qry = torch.from_numpy(np.ascontiguousarray(x[N:])).to(dev)
+    offsets, edges = bench.build_graph(torch, rows[1:], 48, 16, 32, 64, dev)
+    ix = DeviceIndex("l2", "float", D)
+    ix.set_objects_device(rows.data_ptr(), N + 1)
+    ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
+    seeds = bench.random_seeds(N + 1, NQ, 10)
+    d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+    d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * 10
+    rejected = 0
+    for eps, vis in [(0.0, 0), (0.05, -2), (0.1, -1), (0.3, -2)]:
+        on_ = _search(torch, ix, qry, d_seeds, d_soff, NQ, K, eps, vis, 1)
+        off = _search(torch, ix, qry, d_seeds, d_soff, NQ, K, eps, vis, -1)
+        assert on_[4] and not off[4]
+        assert np.array_equal(on_[2], off[2]), (data, eps)
+        assert np.array_equal(on_[0], off[0]), (data, eps)
+        assert np.array_equal(on_[1], off[1]), (data, eps)
+        for col in (0, 1, 2, 4, 5, 7):
+            assert np.array_equal(on_[3][:, col], off[3][:, col]), (data, eps, col)
+        rejected += int((off[3][:, 6] - on_[3][:, 6]).sum())
+    if data == "nonfinite":
+        assert rejected == 0
+    else:
+        assert rejected > 0
+    ix.close()
