@@ -433,6 +433,9 @@ def main():
         log("accepted-only visited set: results identical; %.0f evaluations/query vs %.0f distinct" % (
             evals_per_query, float(cnt[:, 0].double().mean())))
         c = cnt.cpu().numpy().astype(np.float64)
+    ne = c[:, 2]
+    log("expansions/query: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %.0f" % (
+        ne.mean(), np.percentile(ne, 50), np.percentile(ne, 90), np.percentile(ne, 99), ne.max()))
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     graph = "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg)
     if qgm:
@@ -455,9 +458,9 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic, tentry = measured_traffic(args.mode, args.config, graph, chosen, args.visited, filtered)
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
-        tot = c[:, [5, 6, 7, 3]].mean(0)
-        log("phase cycles/query: pop %.3g adjacency+visited %.3g eval %.3g accept+rest %.3g (sum %.3g)" % (
-            tot[0], tot[1], tot[2], tot[3], tot.sum()))
+        tot = c[:, [5, 6, 1, 7, 3]].mean(0)
+        log("phase cycles/query: pop %.3g adjacency+visited %.3g filter %.3g eval %.3g accept+rest %.3g "
+            "(sum %.3g)" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum()))
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "qg":
         tot = c[:, [4, 5, 6, 7]].mean(0)
         log("phase cycles/query: pop %.3g ids %.3g codes+adc %.3g accept %.3g (sum %.3g)" % (

@@ -344,28 +344,36 @@ __device__ __forceinline__ void eval_stream(const float* qlds, const uint8_t* ro
 
 
 // ---------------------------------------------------------------------------
-// Lower bounds from the 1-byte filter copy (filter_kernels.hip): out[r] = the
-// float evaluation of ||q' - b c(r)|| with q' = q - a staged in LDS, i.e. of
-// ||q - x~||; the caller rejects a neighbour when this minus the error margin
-// exceeds the exploration radius.  Quad per row: lane g of a quad takes
-// elements [g E, g E + E), E = dp / 4; up to 64 rows' codes (4 x 16 rows) are
-// in flight before the first FMA.  Not bit-matched to anything: a bound.
+// Lower bounds from the 1-byte filter copy (filter_kernels.hip), in exact
+// integer arithmetic.  With x~ = a + b c (codes c in [0,255]), q' = (q - a)/b,
+// its clamp to [0,255] q^ and the per-query byte vector q'' = rint(q^):
+//   ||q - x|| >= ||q - x~|| - E = b ||q' - c|| - E >= b ||q^ - c|| - E
+//             >= b (||q'' - c|| - r_q) - E,      r_q = ||q^ - q''||
+// (clamping moves q' closer to every code vector; triangle inequality twice).
+// out[r] = S = ||q'' - c(r)||^2 = sum q''^2 + sum c^2 - 2 sum q'' c, exact in
+// u32 via v_dot4_u32_u8; the caller rejects when S exceeds the square of
+// (radius + E)/b + r_q, rounded up.  Quad per row: lane g of a quad takes
+// bytes [g E, g E + E), E = dp / 4; 64 rows' codes (4 x 16 rows) are in
+// flight before the first dot product.  Not bit-matched to anything: a bound.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float quad_sum(float s) {
-  s += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0xb1, 0xf, 0xf, false));  // lane ^ 1
-  s += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x4e, 0xf, 0xf, false));  // lane ^ 2
+__device__ __forceinline__ uint32_t quad_sum_u32(uint32_t s) {
+  s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xb1, 0xf, 0xf, false);  // lane ^ 1
+  s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4e, 0xf, 0xf, false);  // lane ^ 2
   return s;
 }
 
 template <int NCH>
-__device__ __forceinline__ void filter_l2u8(const float* qa, const uint8_t* codes, float b, const uint32_t* ids,
-                                            float* out, int m) {
+__device__ __forceinline__ void filter_l2u8(const uint8_t* qb, uint32_t sq, const uint8_t* codes,
+                                            const uint32_t* ids, uint32_t* out, int m) {
   static_assert((NCH & 1) == 0, "whole 8-byte code words per lane");
-  constexpr int E = 4 * NCH;   // elements per lane
+  constexpr int E = 4 * NCH;   // bytes per lane
   constexpr int NW = E / 8;    // 8-byte code words per lane
   const int lane = lane_id();
   const int g = lane & 3, rs = lane >> 2;
-  const float* q = qa + g * E;
+  uint2 q[NW];
+  const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
+#pragma unroll
+  for (int w = 0; w < NW; w++) q[w] = qp[w];
   for (int r0 = 0; r0 < m; r0 += 64) {
     uint2 c[4][NW];
 #pragma unroll
@@ -379,28 +387,52 @@ __device__ __forceinline__ void filter_l2u8(const float* qa, const uint8_t* code
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (j == 0 || r0 + 16 * j < m) {
-        float acc0 = 0.0f, acc1 = 0.0f;
+        uint32_t qc = 0u, cc = 0u;
 #pragma unroll
         for (int w = 0; w < NW; w++) {
-          const uint32_t lo = c[j][w].x, hi = c[j][w].y;
-          const float4 q0 = *reinterpret_cast<const float4*>(q + 8 * w);
-          const float4 q1 = *reinterpret_cast<const float4*>(q + 8 * w + 4);
-          float d;
-          d = __builtin_fmaf(-b, (float)(lo & 0xffu), q0.x); acc0 = __builtin_fmaf(d, d, acc0);
-          d = __builtin_fmaf(-b, (float)((lo >> 8) & 0xffu), q0.y); acc1 = __builtin_fmaf(d, d, acc1);
-          d = __builtin_fmaf(-b, (float)((lo >> 16) & 0xffu), q0.z); acc0 = __builtin_fmaf(d, d, acc0);
-          d = __builtin_fmaf(-b, (float)(lo >> 24), q0.w); acc1 = __builtin_fmaf(d, d, acc1);
-          d = __builtin_fmaf(-b, (float)(hi & 0xffu), q1.x); acc0 = __builtin_fmaf(d, d, acc0);
-          d = __builtin_fmaf(-b, (float)((hi >> 8) & 0xffu), q1.y); acc1 = __builtin_fmaf(d, d, acc1);
-          d = __builtin_fmaf(-b, (float)((hi >> 16) & 0xffu), q1.z); acc0 = __builtin_fmaf(d, d, acc0);
-          d = __builtin_fmaf(-b, (float)(hi >> 24), q1.w); acc1 = __builtin_fmaf(d, d, acc1);
+          qc = __builtin_amdgcn_udot4(q[w].x, c[j][w].x, qc, false);
+          qc = __builtin_amdgcn_udot4(q[w].y, c[j][w].y, qc, false);
+          cc = __builtin_amdgcn_udot4(c[j][w].x, c[j][w].x, cc, false);
+          cc = __builtin_amdgcn_udot4(c[j][w].y, c[j][w].y, cc, false);
         }
-        const float s = quad_sum(acc0 + acc1);
+        const uint32_t s = quad_sum_u32(cc - 2u * qc);  // modulo 2^32: the total below is exact
         const int r = r0 + 16 * j + rs;
-        if (g == 0 && r < m) out[r] = sqrtf(s);
+        if (g == 0 && r < m) out[r] = sq + s;
       }
     }
   }
+}
+
+// Per-query filter state: q'' bytes into qb (LDS), sum q''^2 and the
+// rounding radius r_q (rounded up); wave-uniform results.
+__device__ __forceinline__ void filter_query(const float* qf, int dp, float fa, float fb, uint8_t* qb, uint32_t& sq,
+                                             double& rq) {
+  uint32_t s = 0u;
+  double r2 = 0.0;
+  for (int i = lane_id(); i < dp; i += 64) {
+    float c = rintf((qf[i] - fa) / fb);
+    c = c >= 0.0f ? (c <= 255.0f ? c : 255.0f) : 0.0f;  // NaN -> 0 (r_q is then NaN: no rejection)
+    qb[i] = (uint8_t)c;
+    s += (uint32_t)c * (uint32_t)c;
+    double t = ((double)qf[i] - (double)fa) / (double)fb;
+    t = t < 0.0 ? 0.0 : (t > 255.0 ? 255.0 : t);
+    r2 += (t - (double)c) * (t - (double)c);
+  }
+  sq = wave_sum_u32(s);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) r2 += __shfl_xor(r2, o, 64);
+  rq = sqrt(r2) * (1.0 + 1e-9) + 1e-9;
+}
+
+// The largest S a neighbour may have and still lie within `expr`: the square
+// of (expr (1 + 2^-15) + E) / b + r_q, rounded up (the 2^-15 covers the
+// comparator's own float rounding); all ones (keep everything) when that is
+// not finite or beyond u32.
+__device__ __forceinline__ uint32_t filter_threshold(float expr, double fe, double inv_b, double rq) {
+  const double t = ((double)expr * (1.0 + 0x1p-15) + fe) * inv_b + rq;
+  const double t2 = t * t * (1.0 + 1e-12) + 1e-6;
+  if (!(t2 < 4294967295.0)) return 0xffffffffu;
+  return (uint32_t)t2;  // floor: S > t2 <=> S > floor(t2) for integer S
 }
 
 }  // namespace ngt_amd

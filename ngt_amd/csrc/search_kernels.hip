@@ -174,6 +174,17 @@ __device__ __forceinline__ void cq_chunk_min(const uint64_t* cq, uint64_t* cmin,
   if (lane_id() == 0) cmin[c] = m;
 }
 
+// One adjacency row of the padded fixed-stride copy, all chunks in one round
+// trip: lane l holds ids l, l + 64, l + 128, l + 192 (0 past `deg`).
+__device__ __forceinline__ void load_adj_row(const uint32_t* row, uint64_t deg, uint32_t& r0, uint32_t& r1,
+                                             uint32_t& r2, uint32_t& r3) {
+  const uint32_t l = (uint32_t)lane_id();
+  r0 = l < deg ? row[l] : 0u;
+  r1 = l + 64 < deg ? row[l + 64] : 0u;
+  r2 = l + 128 < deg ? row[l + 128] : 0u;
+  r3 = l + 192 < deg ? row[l + 192] : 0u;
+}
+
 template <int M, typename T, int NCH, int G>
 __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -201,7 +212,10 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   p += ((size_t)a.dp * sizeof(T) + 15) & ~(size_t)15;
   // 1-byte filter copy (filter_kernels.hip): L2 float rows of dp = 16 * NCH
   constexpr bool kFilterable = NCH > 0 && (NCH & 1) == 0 && M == kL2 && sizeof(T) == 4;
-  float* qa = reinterpret_cast<float*>(p);  // q - a, when filtering
+  uint8_t* qb = p;  // the query's filter bytes q'', when filtering
+  // neighbours of the current expansion whose exact distance is pending, in
+  // neighbour order (64 ids; allocated when filtering)
+  uint32_t* surv = reinterpret_cast<uint32_t*>(p + (size_t)a.dp);
   bool use_filter = false;
   float fa = 0.f, fb = 0.f, fe = 0.f, fx = 0.f;
   if constexpr (kFilterable) {
@@ -211,9 +225,10 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       fb = a.fparams[1];
       fe = a.fparams[2];
       fx = a.fparams[3];
+      use_filter = fb > 0.0f;  // b = 0: every element equals a, nothing to reject
     }
   }
-  (void)qa; (void)fa; (void)fb; (void)fe; (void)fx;
+  (void)qb; (void)surv; (void)fa; (void)fb; (void)fe; (void)fx;
 
   const uint32_t slot = blockIdx.x;
   uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
@@ -243,19 +258,14 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     float qfold = 0.f;
     if constexpr (NCH < 0 && (M == kCosine || M == kAngle))
       qfold = query_sq_fold(reinterpret_cast<const float*>(qlds), a.dp);
-    // filter margin: E plus the float evaluation error of ||q - x~||
-    double fmarg = 0.0;
+    // filter bytes of the query, sum q''^2 and r_q (search_common.h, filter_l2u8)
+    uint32_t fsq = 0u;
+    double frq = 0.0, finv_b = 0.0;
+    (void)fsq; (void)frq; (void)finv_b;
     if constexpr (kFilterable) {
       if (use_filter) {
-        const float* qf = reinterpret_cast<const float*>(qlds);
-        float sq = 0.f;
-        for (int i = lane; i < a.dp; i += 64) {
-          qa[i] = qf[i] - fa;
-          sq = __builtin_fmaf(qf[i], qf[i], sq);
-        }
-        sq = wave_sum_f32(sq);
-        const double qn = sqrt((double)sq) * (1.0 + 1e-5);
-        fmarg = (double)fe + 0x1p-16 * (qn + (double)fx + sqrt((double)a.dp) * fabs((double)fa) + 1.0);
+        filter_query(reinterpret_cast<const float*>(qlds), a.dp, fa, fb, qb, fsq, frq);
+        finv_b = 1.0 / (double)fb;
         __syncthreads();
       }
     }
@@ -265,8 +275,8 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     uint32_t nvisited = 0;
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0, nexact = 0;
-    uint64_t t_pop = 0, t_adj = 0, t_eval = 0, t_last = 0, t_rest = 0;
-    (void)t_pop; (void)t_adj; (void)t_eval; (void)t_last; (void)t_rest;
+    uint64_t t_pop = 0, t_adj = 0, t_filt = 0, t_eval = 0, t_last = 0, t_rest = 0;
+    (void)t_pop; (void)t_adj; (void)t_filt; (void)t_eval; (void)t_last; (void)t_rest;
 #ifdef NGT_AMD_STAMPS
     t_last = stamp();
 #endif
@@ -314,6 +324,64 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     }
     if (nres >= k) radius = key_dist(st.res[k - 1]);
     float expr = __fmul_rn(a.coef, radius);
+
+    // Accept `me` evaluated neighbours (ids[j], distances st.nd[j]) in
+    // neighbour order (Graph.cpp:471-483); only candidates within the radius
+    // at batch start can be accepted.
+    auto accept_batch = [&](const uint32_t* ids, uint32_t me) {
+      uint64_t okmask = ballot64((uint32_t)lane < me && st.nd[lane] <= expr);
+      while (okmask) {
+        const int j = __ffsll((long long)okmask) - 1;
+        okmask &= okmask - 1;
+        const float d = st.nd[j];
+        if (!(d <= expr)) continue;
+        const uint64_t key = make_key(d, ids[j]);
+        if (lazy && lane == 0) mark_accepted(st, ids[j], vis, epoch);
+        if (ncq >= a.cq_cap) {
+          ncq = compact(st.cq, ncq, expr);
+          if (nspill) nspill = compact(spill, nspill, expr);
+          for (uint32_t c = 0; c < ((ncq + 63) >> 6); c++) cq_chunk_min(st.cq, cmin, ncq, c);
+          __builtin_amdgcn_wave_barrier();
+        }
+        if (ncq < a.cq_cap) {
+          if (lane == 0) {
+            st.cq[ncq] = key;
+            const uint32_t c = ncq >> 6;
+            cmin[c] = (ncq & 63) == 0 ? key : (key < cmin[c] ? key : cmin[c]);
+          }
+          ncq++;
+        } else {
+          if (nspill >= a.spill_cap) {
+            if (lane == 0) atomicOr(a.error, 1);
+          } else {
+            if (lane == 0) spill[nspill] = key;
+            nspill++;
+          }
+        }
+        if (ncq + nspill > maxq) maxq = ncq + nspill;  // the largest unchecked set
+        if (d <= radius) {
+          res_insert(st.res, nres, k, key);
+          if (nres >= k) {
+            radius = key_dist(st.res[k - 1]);
+            expr = __fmul_rn(a.coef, radius);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      __syncthreads();
+      // exact overflow of the visited set into the HBM bitmap
+      if (!bitmap_mode && nvisited > hlimit) {
+        ht_to_vis(a.ht_log2, st, vis, epoch);
+        bitmap_mode = true;
+        __syncthreads();
+      }
+    };
+
+    // Adjacency row prefetch (filtered accepted-only mode): after each pop the
+    // row of the next key in line is loaded under the current expansion and
+    // used when that key is the next pop (nothing closer was accepted).
+    uint32_t pf_node = 0, pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0;
+    (void)pf_node; (void)pf0; (void)pf1; (void)pf2; (void)pf3;
 
     // ---- best-first loop (Graph.cpp:430-486) ----------------------------
     for (;;) {
@@ -379,6 +447,90 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         if (deg > a.edge_size) deg = a.edge_size;
       }
 
+      if constexpr (kFilterable) {
+        if (use_filter && lazy && padded && deg <= 256) {
+          // Pipelined expansion.  Round trips: the row's ids (none when
+          // prefetched), then the filter codes of a 64-id chunk together with
+          // the epoch bytes of its filter-positive ids, then one exact-row
+          // batch for the survivors of every chunk.  Deferring the exact
+          // distances past later chunks only widens the filter threshold
+          // those chunks see (the radius never grows), and the survivors are
+          // accepted in neighbour order with the current radius: the
+          // traversal is the same.
+          const uint32_t nchk = (uint32_t)((deg + 63) >> 6);
+          uint32_t a0, a1, a2, a3;
+          if (pf_node == target) {
+            a0 = pf0; a1 = pf1; a2 = pf2; a3 = pf3;
+          } else {
+            load_adj_row(a.adj + eb, deg, a0, a1, a2, a3);
+          }
+          // the next key in line: the minimum left after this pop
+          {
+            uint64_t nb = ~0ull;
+            const uint32_t nc2 = (ncq + 63) >> 6;
+            if ((uint32_t)lane < nc2) nb = cmin[lane];
+            if ((uint32_t)lane + 64 < nc2) { const uint64_t v = cmin[lane + 64]; nb = v < nb ? v : nb; }
+            for (uint32_t i = lane; i < nspill; i += 64) { const uint64_t v = spill[i]; nb = v < nb ? v : nb; }
+            nb = wave_min_u64(nb);
+            pf_node = (nb != ~0ull && key_dist(nb) <= expr) ? key_id(nb) : 0u;
+            if (pf_node) load_adj_row(a.adj + (uint64_t)pf_node * a.adj_stride, deg, pf0, pf1, pf2, pf3);
+          }
+          NGT_MARK(t_adj);
+          uint32_t ns = 0;
+          for (uint32_t c = 0; c < nchk; c++) {
+            const uint32_t id = c == 0 ? a0 : (c == 1 ? a1 : (c == 2 ? a2 : a3));
+            const uint64_t vmask = ballot64(id != 0u);
+            const uint32_t cnt = (uint32_t)__popcll(vmask);  // 0-terminated: a prefix
+            nedge += cnt;
+            if (cnt == 0) break;
+            // accepted-only visited test: a clear filter bit proves the id
+            // fresh; a set bit needs its epoch byte, loaded with the codes
+            bool bit = false;
+            uint32_t pw = 0;
+            if (id != 0u) {
+              const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+              bit = ((st.vf[b >> 5] >> (b & 31)) & 1u) != 0u;
+              if (bit)
+                pw = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            st.nid[lane] = id;
+            __syncthreads();
+            filter_l2u8<NCH>(qb, fsq, a.fcodes, st.nid, reinterpret_cast<uint32_t*>(st.nd), (int)cnt);
+            __syncthreads();
+            const bool fresh = id != 0u && (!bit || ((pw >> (8 * (id & 3))) & 0xffu) != epoch);
+            const uint32_t m = (uint32_t)__popcll(ballot64(fresh));
+            ndist += m;
+            nvisit += m;
+            nvisited += m;
+            const uint32_t fthr = filter_threshold(expr, (double)fe, finv_b, frq);
+            const bool keep = fresh && reinterpret_cast<const uint32_t*>(st.nd)[lane] <= fthr;
+            const uint64_t km = ballot64(keep);
+            const uint32_t me = (uint32_t)__popcll(km);
+            nexact += me;
+            NGT_MARK(t_filt);
+            if (ns + me > 64) {
+              eval_any<M, T, NCH, G>(qlds, a, qfold, surv, st.nd, (int)ns);
+              __syncthreads();
+              NGT_MARK(t_eval);
+              accept_batch(surv, ns);
+              ns = 0;
+            }
+            if (keep) surv[ns + mbcnt(km)] = id;
+            ns += me;
+            __syncthreads();
+            if (cnt < 64) break;
+          }
+          if (ns != 0) {
+            eval_any<M, T, NCH, G>(qlds, a, qfold, surv, st.nd, (int)ns);
+            __syncthreads();
+            NGT_MARK(t_eval);
+            accept_batch(surv, ns);
+          }
+          continue;
+        }
+      }
+
       for (uint64_t base = 0; base < deg; base += 64) {
         const uint32_t cnt = (uint32_t)(deg - base < 64 ? deg - base : 64);
         uint32_t id = 0;
@@ -399,10 +551,10 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         uint32_t me = m;
         if constexpr (kFilterable) {
           if (use_filter && m != 0) {
-            filter_l2u8<NCH>(qa, a.fcodes, fb, st.nid, st.nd, (int)m);
+            filter_l2u8<NCH>(qb, fsq, a.fcodes, st.nid, reinterpret_cast<uint32_t*>(st.nd), (int)m);
             __syncthreads();
-            const double fthr = (double)expr * (1.0 + 0x1p-15) + fmarg;
-            const bool keep = (uint32_t)lane < m && !((double)st.nd[lane] > fthr);
+            const uint32_t fthr = filter_threshold(expr, (double)fe, finv_b, frq);
+            const bool keep = (uint32_t)lane < m && reinterpret_cast<const uint32_t*>(st.nd)[lane] <= fthr;
             const uint32_t myid = (uint32_t)lane < m ? st.nid[lane] : 0u;
             const uint64_t km = ballot64(keep);
             __syncthreads();
@@ -411,6 +563,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
             __syncthreads();
           }
         }
+        NGT_MARK(t_filt);
         ndist += m;
         nvisit += m;
         nexact += me;
@@ -418,54 +571,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
           eval_any<M, T, NCH, G>(qlds, a, qfold, st.nid, st.nd, (int)me);
           __syncthreads();
           NGT_MARK(t_eval);
-          // accept in neighbour order (Graph.cpp:471-483); only candidates
-          // within the radius at batch start can be accepted.
-          uint64_t okmask = ballot64((uint32_t)lane < me && st.nd[lane] <= expr);
-          while (okmask) {
-            const int j = __ffsll((long long)okmask) - 1;
-            okmask &= okmask - 1;
-            const float d = st.nd[j];
-            if (!(d <= expr)) continue;
-            const uint64_t key = make_key(d, st.nid[j]);
-            if (lazy && lane == 0) mark_accepted(st, st.nid[j], vis, epoch);
-            if (ncq >= a.cq_cap) {
-              ncq = compact(st.cq, ncq, expr);
-              if (nspill) nspill = compact(spill, nspill, expr);
-              for (uint32_t c = 0; c < ((ncq + 63) >> 6); c++) cq_chunk_min(st.cq, cmin, ncq, c);
-              __builtin_amdgcn_wave_barrier();
-            }
-            if (ncq < a.cq_cap) {
-              if (lane == 0) {
-                st.cq[ncq] = key;
-                const uint32_t c = ncq >> 6;
-                cmin[c] = (ncq & 63) == 0 ? key : (key < cmin[c] ? key : cmin[c]);
-              }
-              ncq++;
-            } else {
-              if (nspill >= a.spill_cap) {
-                if (lane == 0) atomicOr(a.error, 1);
-              } else {
-                if (lane == 0) spill[nspill] = key;
-                nspill++;
-              }
-            }
-            if (d <= radius) {
-              res_insert(st.res, nres, k, key);
-              if (nres >= k) {
-                radius = key_dist(st.res[k - 1]);
-                expr = __fmul_rn(a.coef, radius);
-              }
-            }
-            __builtin_amdgcn_wave_barrier();
-          }
-          if (ncq + nspill > maxq) maxq = ncq + nspill;
-          __syncthreads();
-          // exact overflow of the visited set into the HBM bitmap
-          if (!bitmap_mode && nvisited > hlimit) {
-            ht_to_vis(a.ht_log2, st, vis, epoch);
-            bitmap_mode = true;
-            __syncthreads();
-          }
+          accept_batch(st.nid, me);
         }
         if (padded && vmask != ~0ull) break;  // 0-terminated list ended in this chunk
       }
@@ -490,6 +596,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         c[6] = t_adj;
         c[7] = t_eval;
         c[3] = t_rest;  // accept + loop overhead
+        c[1] = t_filt;  // filter codes + bound (0 without the filter)
 #else
         c[5] = maxq;
         c[6] = use_filter ? nexact : ndist - (ns < ndist ? ns : ndist);  // exact distances of neighbours
@@ -729,7 +836,7 @@ size_t search_lds_bytes(const SearchArgs& a, int otype) {
   b += ((size_t)8 * (a.k + 1) + 15) & ~(size_t)15;
   b += 512;
   b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
-  if (a.fcodes) b += (size_t)a.dp * 4;  // q - a for the filter
+  if (a.fcodes) b += (size_t)a.dp + 256;  // the query's filter bytes and the pending survivors
   return b;
 }
 
