@@ -206,6 +206,10 @@ def main():
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--target", type=float, default=0.95)
+    ap.add_argument("--graph", choices=["knn", "anng"], default="knn",
+                    help="knn: exact kNN graph built in setup (out/in edges); anng: this library's own "
+                         "ngt_create_index ANNG (GraphAndTreeIndex::createIndex on the device)")
+    ap.add_argument("--anng-edges", type=int, default=10, help="--graph anng: edgeSizeForCreation (ngt create -E)")
     ap.add_argument("--knn", type=int, default=128)
     ap.add_argument("--out-deg", type=int, default=48)
     ap.add_argument("--in-deg", type=int, default=96)
@@ -271,11 +275,23 @@ def main():
     rows = torch.zeros((N + 1, dp), dtype=torch.float32, device=dev)
     rows[1:, :D] = torch.from_numpy(base).to(dev)
     qraw = torch.from_numpy(qry).to(dev)
-    offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev,
-                                 cosine=c3)
-
     ix = DeviceIndex(metric, "float", D, device=local)
     ix.set_objects_device(rows.data_ptr(), N + 1)
+    build_s = None
+    if args.graph == "anng":
+        # the index a user of `ngt create -g a -E <e>` gets, built by this
+        # library's own device construction (byte-identical to the
+        # reference's at C1, tests/test_gpu_build.py)
+        t0 = time.time()
+        (h_off, h_ids, _), _tree = ix.build_anng(edge_size_for_creation=args.anng_edges)
+        build_s = time.time() - t0
+        offsets = torch.from_numpy(h_off.astype(np.int64)).to(dev)
+        edges = torch.from_numpy(h_ids.astype(np.int32)).to(dev)
+        log("ANNG (E=%d) built on the device in %.1f s: %d edges, mean degree %.1f" % (
+            args.anng_edges, build_s, edges.numel(), edges.numel() / N))
+    else:
+        offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev,
+                                     cosine=c3)
     ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
     ix.set_search_property(0, 30, 20, args.seed_size, 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -437,7 +453,8 @@ def main():
     log("expansions/query: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %.0f" % (
         ne.mean(), np.percentile(ne, 50), np.percentile(ne, 90), np.percentile(ne, 99), ne.max()))
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
-    graph = "kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg)
+    graph = ("kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg) if args.graph == "knn"
+             else "ANNG E%d (ngt_create_index on the device)" % args.anng_edges)
     if qgm:
         # B(q) = sum_exp ceil(deg/16)*16*(M/2) + deg*4 + (seeds + k*expansion)*Dp*4  
         me = (D + 1) // 2 * 2
@@ -533,6 +550,8 @@ def main():
         }
         if scan is not None:
             line["exact_scan"] = scan
+        if build_s is not None:
+            line["config"]["graph_build_s"] = build_s
         cn = tentry.get("counters_per_launch")
         if cn:
             # PMC evidence for what bounds the kernel (profiles/traffic.json):
@@ -548,6 +567,8 @@ def main():
             line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
         else:
             line["config"]["edges_read_per_query"] = float(c[:, 4].mean())
+            line["config"]["adjacency_prefetch_hits_per_expansion"] = float(
+                (c[:, 3].astype(np.int64) >> 1).sum() / max(1.0, c[:, 2].sum()))
             if filtered:
                 line["config"]["exact_neighbour_distances_per_query"] = float(c[:, 6].mean())
             if evals_per_query is not None:
