@@ -543,7 +543,11 @@ def main():
                        "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
-                         "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes},
+                         "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes,
+                         # the same bytes over the whole step with launches overlapping on the streams
+                         # (a single launch's last round of queries leaves the GPU part-empty)
+                         "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
+                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "sweep": sweep,
@@ -567,8 +571,6 @@ def main():
             line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
         else:
             line["config"]["edges_read_per_query"] = float(c[:, 4].mean())
-            line["config"]["adjacency_prefetch_hits_per_expansion"] = float(
-                (c[:, 3].astype(np.int64) >> 1).sum() / max(1.0, c[:, 2].sum()))
             if filtered:
                 line["config"]["exact_neighbour_distances_per_query"] = float(c[:, 6].mean())
             if evals_per_query is not None:

@@ -277,7 +277,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
           ex += (double)h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + 2];
           mx = std::max(mx, h_cnt[(size_t)i * NGT_AMD_COUNTERS_PER_QUERY + 2]);
           const uint64_t* c = h_cnt.data() + (size_t)i * NGT_AMD_COUNTERS_PER_QUERY;
-          c3 += (double)(c[3] >> 1);  // adjacency prefetch hits
+          c3 += (double)c[3];
           c5 += (double)c[5];
           c6 += (double)c[6];
           c7 += (double)c[7];

@@ -274,7 +274,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     const bool lazy = a.accepted_only && !use_hash && st.vf;
     uint32_t nvisited = 0;
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
-    uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0, nexact = 0, npf = 0;
+    uint64_t ndist = 0, nvisit = 0, nexp = 0, nedge = 0, nexact = 0;
     uint64_t t_pop = 0, t_adj = 0, t_filt = 0, t_eval = 0, t_last = 0, t_rest = 0;
     (void)t_pop; (void)t_adj; (void)t_filt; (void)t_eval; (void)t_last; (void)t_rest;
 #ifdef NGT_AMD_STAMPS
@@ -461,7 +461,6 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
           uint32_t a0, a1, a2, a3;
           if (pf_node == target) {
             a0 = pf0; a1 = pf1; a2 = pf2; a3 = pf3;
-            npf++;
           } else {
             load_adj_row(a.adj + eb, deg, a0, a1, a2, a3);
           }
@@ -590,7 +589,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         c[0] = ndist;
         c[1] = nvisit;
         c[2] = nexp;
-        c[3] = ((bitmap_mode && use_hash) ? 1 : 0) | npf << 1;  // bit 0: hash overflowed; adjacency prefetch hits
+        c[3] = (bitmap_mode && use_hash) ? 1 : 0;
         c[4] = nedge;
 #ifdef NGT_AMD_STAMPS
         c[5] = t_pop;

@@ -265,7 +265,7 @@ def test_overflow_paths_exact(monkeypatch, ht, cq, adj, vf, dim):
             assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32))
             assert int(cnt[i, 0]) == int(ocnt[0])
         if ht == "8" and eps == 1.0:
-            assert (cnt[:, 3] & 1).sum() > 0  # the bitmap path really ran
+            assert cnt[:, 3].sum() > 0  # the bitmap path really ran
     ix.close()
 
 

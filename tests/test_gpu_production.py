@@ -170,3 +170,36 @@ def test_distance_filter_identical(data):
     else:
         assert rejected > 0
     ix.close()
+
+
+def test_distance_filter_small_launches():
+    """Single-query-sized launches (the C API's coalesced calls) take the
+    pipelined filtered expansion with the full visited set as well as the
+    accepted-only one: ids, distance bits, result counts and the reference's
+    counters equal the unfiltered search."""
+    import torch
+    import bench
+    dev = torch.device("cuda:0")
+    N, D, NQ, K = 60_000, 128, 64, 10
+    x = bench.splitmix_uniform(N + NQ, D, bench.BASE_SEED + 11)
+    rows = torch.zeros((N + 1, D), dtype=torch.float32, device=dev)
+    rows[1:] = torch.from_numpy(x[:N]).to(dev)
+    qry = torch.from_numpy(np.ascontiguousarray(x[N:])).to(dev)
+    offsets, edges = bench.build_graph(torch, rows[1:], 48, 16, 32, 64, dev)
+    ix = DeviceIndex("l2", "float", D)
+    ix.set_objects_device(rows.data_ptr(), N + 1)
+    ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
+    seeds = bench.random_seeds(N + 1, NQ, 10)
+    d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+    d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * 10
+    for nq in (1, 7, 64):
+        for eps, vis in [(0.05, -1), (0.1, -2), (0.0, -1)]:
+            on_ = _search(torch, ix, qry[:nq], d_seeds, d_soff, nq, K, eps, vis, 1)
+            off = _search(torch, ix, qry[:nq], d_seeds, d_soff, nq, K, eps, vis, -1)
+            assert on_[4] and not off[4]
+            assert np.array_equal(on_[2], off[2]), (nq, eps, vis)
+            assert np.array_equal(on_[0], off[0]), (nq, eps, vis)
+            assert np.array_equal(on_[1], off[1]), (nq, eps, vis)
+            for col in (0, 1, 2, 4, 5, 7):
+                assert np.array_equal(on_[3][:, col], off[3][:, col]), (nq, eps, vis, col)
+    ix.close()
