@@ -484,8 +484,12 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       const char* v = getenv("NGT_AMD_FILTER");
       return v ? atoi(v) : -1;
     }();
-    const bool shape = ix->metric == NGT_AMD_DISTANCE_L2 && ix->otype == NGT_AMD_OBJECT_FLOAT &&
-                       (ix->dp == 128 || ix->dp == 96);
+    // L2 rows of 96/128 floats (integer bound, pipelined expansion) or
+    // cosine/angle long rows (streamed comparator; search_common.h filter_cos_u8)
+    const bool shape = ix->otype == NGT_AMD_OBJECT_FLOAT &&
+                       ((ix->metric == NGT_AMD_DISTANCE_L2 && (ix->dp == 128 || ix->dp == 96)) ||
+                        ((ix->metric == NGT_AMD_DISTANCE_COSINE || ix->metric == NGT_AMD_DISTANCE_ANGLE) &&
+                         ix->dp > 128 && ix->dp % 64 == 0 && !getenv("NGT_AMD_NO_STREAM")));
     const bool want = force >= 0 ? force != 0
                                  : (prm->distance_filter != 0 ? prm->distance_filter > 0
                                                               : nq >= 2u * (uint32_t)ix->cu_count);

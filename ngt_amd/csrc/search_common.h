@@ -32,6 +32,14 @@ __device__ __forceinline__ uint64_t stamp() {
 #define NGT_MARK(dst)
 #endif
 
+// a wave-uniform double kept in SGPRs (the shuffle reductions leave the same
+// value in every lane, which the compiler cannot see)
+__device__ __forceinline__ double uniform_f64(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
 template <typename T>
 __device__ __forceinline__ const T* row_ptr(const uint8_t* rows, uint64_t row_bytes, uint32_t id) {
   return reinterpret_cast<const T*>(rows + (uint64_t)id * row_bytes);
@@ -433,6 +441,123 @@ __device__ __forceinline__ uint32_t filter_threshold(float expr, double fe, doub
   const double t2 = t * t * (1.0 + 1e-12) + 1e-6;
   if (!(t2 < 4294967295.0)) return 0xffffffffu;
   return (uint32_t)t2;  // floor: S > t2 <=> S > floor(t2) for integer S
+}
+
+// ---------------------------------------------------------------------------
+// Cosine / angle lower bounds from the 1-byte filter copy (long rows, Dp a
+// multiple of 64).  With x = x~ + e, |e| <= E, x~ = a + b c, and the query
+// split as q = a + b q'' + r (q'' = rint(clamp((q - a)/b)), r the residual):
+//   q.x  <= q.x~ + |q| E,   |x| >= |x~| - E,
+//   q.x~ =  a sum q + b (a sum c + b sum q''c + r.c),  r.c <= |r| |c|,
+//   |x~|^2 = Dp a^2 + 2ab sum c + b^2 sum c^2,
+// so cos(q, x) <= U = (q.x~ + |q| E) / (|q| (|x~| - E)) (1 when |x~| <= E).
+// The comparator's float sums (PrimitiveComparator.h:487-553: 16 lanes of
+// Dp/16 FMAs and a 16->1 fold) sit within 8e-6 of the real cosine; with 2e-5
+// of slack the distance is at least 1 - (U + 2e-5) (cosine) or
+// acos(min(1, U + 2e-5)) (angle), stored rounded down.  sum c, sum c^2 and
+// sum q''c are exact u32 sums of v_dot4_u32_u8; 16 lanes per row, dword d of
+// a row on lane d mod 16 (64 contiguous bytes per row per load instruction),
+// 8 rows per wave step.  A bound, not bit-matched to anything.
+// ---------------------------------------------------------------------------
+struct CosFilterQuery {
+  double sum_q;  // sum q_i
+  double qn;     // |q|
+  double rn;     // |q - a - b q''|
+};
+
+__device__ __forceinline__ void filter_query_cos(const float* qf, int dp, float fa, float fb, uint8_t* qb,
+                                                 CosFilterQuery& fq) {
+  double sq = 0.0, qq = 0.0, rr = 0.0;
+  for (int i = lane_id(); i < dp; i += 64) {
+    float c = rintf((qf[i] - fa) / fb);
+    c = c >= 0.0f ? (c <= 255.0f ? c : 255.0f) : 0.0f;  // NaN -> 0 (the sums are then NaN: no rejection)
+    qb[i] = (uint8_t)c;
+    const double q = (double)qf[i];
+    const double r = q - ((double)fa + (double)fb * (double)c);
+    sq += q;
+    qq += q * q;
+    rr += r * r;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    sq += __shfl_xor(sq, o, 64);
+    qq += __shfl_xor(qq, o, 64);
+    rr += __shfl_xor(rr, o, 64);
+  }
+  fq.sum_q = uniform_f64(sq);
+  fq.qn = uniform_f64(sqrt(qq));
+  fq.rn = uniform_f64(sqrt(rr) * (1.0 + 1e-9) + 1e-12);
+}
+
+template <int M>
+__device__ __forceinline__ float cos_filter_bound(uint32_t sc, uint32_t scc, uint32_t sqc, int dp, float fa, float fb,
+                                                  float fe, const CosFilterQuery& fq) {
+  const double a = fa, b = fb, e = fe;
+  const double cn = sqrt((double)scc);
+  const double qx = a * fq.sum_q + b * (a * (double)sc + b * (double)sqc + fq.rn * cn);
+  const double x2 = (double)dp * a * a + 2.0 * a * b * (double)sc + b * b * (double)scc;
+  const double xn = sqrt(x2 > 0.0 ? x2 : 0.0);
+  double u = 1.0;
+  if (xn > e * (1.0 + 1e-9) && fq.qn > 0.0) {
+    const double num = qx * (1.0 + 1e-12) + fabs(qx) * 1e-12 + fq.qn * e;
+    u = num >= 0.0 ? num / (fq.qn * (xn - e) * (1.0 - 1e-12)) : num / (fq.qn * (xn + e) * (1.0 + 1e-12));
+    u += 2e-5;
+  }
+  if (!(u < 1.0)) u = 1.0;  // NaN included
+  if (u < -1.0) u = -1.0;
+  const double lb = M == kCosine ? 1.0 - u : acos(u);
+  return __double2float_rd(lb * (1.0 - 1e-12));
+}
+
+template <int M>
+__device__ __forceinline__ void filter_cos_u8(const uint8_t* qb, const uint8_t* codes, int dp, const uint32_t* ids,
+                                              float* out, int m, float fa, float fb, float fe,
+                                              const CosFilterQuery& fq) {
+  const int lane = lane_id();
+  const int g = lane & 15, rs = lane >> 4;  // 4 rows per 64 lanes
+  const int nw = dp >> 6;                   // dwords per lane per row
+  const uint32_t* qw = reinterpret_cast<const uint32_t*>(qb);
+  for (int r0 = 0; r0 < m; r0 += 8) {
+    const int ra = r0 + rs, rb = r0 + 4 + rs;
+    const uint32_t* xa = reinterpret_cast<const uint32_t*>(codes + (uint64_t)(ra < m ? ids[ra] : 0u) * dp);
+    const uint32_t* xb = reinterpret_cast<const uint32_t*>(codes + (uint64_t)(rb < m ? ids[rb] : 0u) * dp);
+    uint32_t sca = 0u, scca = 0u, sqca = 0u, scb = 0u, sccb = 0u, sqcb = 0u;
+    // blocks of 16 dwords per lane: every load of both rows issued before
+    // the first dot product (Dp = 960: one block, one round trip)
+    for (int kb = 0; kb < nw; kb += 16) {
+      uint32_t ca[16], cb[16];
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const int w = g + 16 * (kb + t);
+        ca[t] = kb + t < nw ? xa[w] : 0u;
+        cb[t] = kb + t < nw ? xb[w] : 0u;
+      }
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const uint32_t q = kb + t < nw ? qw[g + 16 * (kb + t)] : 0u;
+        sca = __builtin_amdgcn_udot4(ca[t], 0x01010101u, sca, false);
+        scca = __builtin_amdgcn_udot4(ca[t], ca[t], scca, false);
+        sqca = __builtin_amdgcn_udot4(q, ca[t], sqca, false);
+        scb = __builtin_amdgcn_udot4(cb[t], 0x01010101u, scb, false);
+        sccb = __builtin_amdgcn_udot4(cb[t], cb[t], sccb, false);
+        sqcb = __builtin_amdgcn_udot4(q, cb[t], sqcb, false);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+      sca += __shfl_xor(sca, o, 16);
+      scca += __shfl_xor(scca, o, 16);
+      sqca += __shfl_xor(sqca, o, 16);
+      scb += __shfl_xor(scb, o, 16);
+      sccb += __shfl_xor(sccb, o, 16);
+      sqcb += __shfl_xor(sqcb, o, 16);
+    }
+    // lane 0 of a 16-lane group bounds its row a, lane 1 its row b
+    const bool isb = g == 1;
+    const int r = isb ? rb : ra;
+    if (g < 2 && r < m)
+      out[r] = cos_filter_bound<M>(isb ? scb : sca, isb ? sccb : scca, isb ? sqcb : sqca, dp, fa, fb, fe, fq);
+  }
 }
 
 }  // namespace ngt_amd

@@ -212,13 +212,15 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   p += ((size_t)a.dp * sizeof(T) + 15) & ~(size_t)15;
   // 1-byte filter copy (filter_kernels.hip): L2 float rows of dp = 16 * NCH
   constexpr bool kFilterable = NCH > 0 && (NCH & 1) == 0 && M == kL2 && sizeof(T) == 4;
+  // cosine / angle bounds for long float rows (streamed comparator)
+  constexpr bool kFilterCos = NCH < 0 && (M == kCosine || M == kAngle) && sizeof(T) == 4;
   uint8_t* qb = p;  // the query's filter bytes q'', when filtering
   // neighbours of the current expansion whose exact distance is pending, in
   // neighbour order (64 ids; allocated when filtering)
   uint32_t* surv = reinterpret_cast<uint32_t*>(p + (size_t)a.dp);
   bool use_filter = false;
   float fa = 0.f, fb = 0.f, fe = 0.f, fx = 0.f;
-  if constexpr (kFilterable) {
+  if constexpr (kFilterable || kFilterCos) {
     if (a.fcodes != nullptr && a.fparams[4] != 0.0f) {
       use_filter = true;
       fa = a.fparams[0];
@@ -266,6 +268,14 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       if (use_filter) {
         filter_query(reinterpret_cast<const float*>(qlds), a.dp, fa, fb, qb, fsq, frq);
         finv_b = 1.0 / (double)fb;
+        __syncthreads();
+      }
+    }
+    CosFilterQuery fcq{};
+    (void)fcq;
+    if constexpr (kFilterCos) {
+      if (use_filter) {
+        filter_query_cos(reinterpret_cast<const float*>(qlds), a.dp, fa, fb, qb, fcq);
         __syncthreads();
       }
     }
@@ -555,6 +565,19 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
             __syncthreads();
             const uint32_t fthr = filter_threshold(expr, (double)fe, finv_b, frq);
             const bool keep = (uint32_t)lane < m && reinterpret_cast<const uint32_t*>(st.nd)[lane] <= fthr;
+            const uint32_t myid = (uint32_t)lane < m ? st.nid[lane] : 0u;
+            const uint64_t km = ballot64(keep);
+            __syncthreads();
+            if (keep) st.nid[mbcnt(km)] = myid;
+            me = (uint32_t)__popcll(km);
+            __syncthreads();
+          }
+        }
+        if constexpr (kFilterCos) {
+          if (use_filter && m != 0) {
+            filter_cos_u8<M>(qb, a.fcodes, a.dp, st.nid, st.nd, (int)m, fa, fb, fe, fcq);
+            __syncthreads();
+            const bool keep = (uint32_t)lane < m && !(st.nd[lane] > expr);
             const uint32_t myid = (uint32_t)lane < m ? st.nid[lane] : 0u;
             const uint64_t km = ballot64(keep);
             __syncthreads();

@@ -203,3 +203,45 @@ def test_distance_filter_small_launches():
             for col in (0, 1, 2, 4, 5, 7):
                 assert np.array_equal(on_[3][:, col], off[3][:, col]), (nq, eps, vis, col)
     ix.close()
+
+
+@pytest.mark.parametrize("metric,D", [("cosine", 192), ("cosine", 960), ("angle", 192)])
+def test_cosine_filter_identical(metric, D):
+    """Long-row cosine / angle searches with the 1-byte filter copy (upper
+    bound of the cosine from code sums, search_common.h filter_cos_u8) return
+    the ids, distance bits, result counts and reference counters of the
+    unfiltered search, on U[0,1) rows and SIFT-like integer rows with an
+    offset."""
+    import torch
+    import bench
+    dev = torch.device("cuda:0")
+    N, NQ, K = (12_000 if D > 256 else 30_000), 256, 10
+    for data in ("uniform", "sift_like"):
+        x = bench.splitmix_uniform(N + NQ, D, bench.BASE_SEED + 13)
+        if data != "uniform":
+            x = np.floor(x * 256.0).astype(np.float32) - 37.0
+        rows = torch.zeros((N + 1, D), dtype=torch.float32, device=dev)
+        rows[1:] = torch.from_numpy(x[:N]).to(dev)
+        qry = torch.from_numpy(np.ascontiguousarray(x[N:])).to(dev)
+        offsets, edges = bench.build_graph(torch, rows[1:], 48, 16, 32, 64, dev, cosine=True)
+        ix = DeviceIndex(metric, "float", D)
+        ix.set_objects_device(rows.data_ptr(), N + 1)
+        ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
+        seeds = bench.random_seeds(N + 1, NQ, 10)
+        d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+        d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * 10
+        rejected = 0
+        for eps, vis in [(0.0, -1), (0.05, -2), (0.1, -1), (0.02, 0)]:
+            on_ = _search(torch, ix, qry, d_seeds, d_soff, NQ, K, eps, vis, 1)
+            off = _search(torch, ix, qry, d_seeds, d_soff, NQ, K, eps, vis, -1)
+            assert on_[4] and not off[4]
+            assert np.array_equal(on_[2], off[2]), (data, eps)
+            assert np.array_equal(on_[0], off[0]), (data, eps)
+            assert np.array_equal(on_[1], off[1]), (data, eps)
+            for col in (0, 1, 2, 4, 5, 7):
+                assert np.array_equal(on_[3][:, col], off[3][:, col]), (data, eps, col)
+            rejected += int((off[3][:, 6] - on_[3][:, 6]).sum())
+        assert rejected > 0, data
+        ix.close()
+        del rows
+        torch.cuda.empty_cache()
