@@ -60,14 +60,14 @@ __device__ __forceinline__ void filter_ab(const uint32_t* st, float& a, float& b
 
 // one thread per row: codes, reconstruction error, norm of the reconstruction
 __global__ void __launch_bounds__(256) ngt_filter_encode_kernel(const uint8_t* rows, uint64_t row_bytes,
-                                                                uint64_t nrows, uint32_t dp, uint8_t* codes,
-                                                                uint32_t* st) {
+                                                                uint64_t nrows, uint32_t dp, uint64_t stride,
+                                                                uint8_t* codes, uint32_t* st) {
   float a, b;
   filter_ab(st, a, b);
   float emax = 0.0f, xmax = 0.0f;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (uint64_t)gridDim.x * blockDim.x) {
     const float* x = reinterpret_cast<const float*>(rows + r * row_bytes);
-    uint32_t* out = reinterpret_cast<uint32_t*>(codes + r * dp);
+    uint32_t* out = reinterpret_cast<uint32_t*>(codes + r * stride);
     double e2 = 0.0, n2 = 0.0;
     for (uint32_t i0 = 0; i0 < dp; i0 += 4) {
       uint32_t w = 0;
@@ -109,8 +109,8 @@ __global__ void ngt_filter_finalize_kernel(const uint32_t* st, float* params) {
   params[4] = st[2] ? 0.0f : 1.0f;
 }
 
-hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint8_t* codes,
-                               uint32_t* st, float* params, hipStream_t s) {
+hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint64_t stride,
+                               uint8_t* codes, uint32_t* st, float* params, hipStream_t s) {
   hipError_t e = hipMemsetAsync(st, 0xff, sizeof(uint32_t), s);
   if (e == hipSuccess) e = hipMemsetAsync(st + 1, 0, 4 * sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
@@ -119,7 +119,7 @@ hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t
     uint64_t blocks = (nrows + 255) / 256;
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(ngt_filter_encode_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, rows, row_bytes, nrows, dp,
-                       codes, st);
+                       stride, codes, st);
   }
   hipLaunchKernelGGL(ngt_filter_finalize_kernel, dim3(1), dim3(64), 0, s, st, params);
   return hipGetLastError();

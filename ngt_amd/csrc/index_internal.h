@@ -202,6 +202,7 @@ struct ngt_amd_index {
     DevBuf<uint8_t> codes;
     DevBuf<uint32_t> st;
     DevBuf<float> params;        // {a, b, E, X, valid}
+    uint64_t stride = 0;         // bytes per code row
     uint64_t version = ~0ull;
   } filt;
   std::vector<uint8_t> h_valid;

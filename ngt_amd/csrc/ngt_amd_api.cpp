@@ -373,10 +373,13 @@ int ngt_amd::run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queri
 static int ensure_filter(ngt_amd_index* ix) {
   std::lock_guard<std::mutex> lk(ix->mu);
   if (ix->filt.version == ix->rows_version) return 0;
-  HIP_OK(ix->filt.codes.alloc((size_t)ix->nrows * ix->dp));
+  // L2 rows of 96/128 elements: dense rows (the search kernel's quads take dp
+  // bytes per row); long rows: rows padded to whole 128-B lines
+  ix->filt.stride = ix->dp <= 128 ? ix->dp : (ix->dp + 127) / 128 * 128;
+  HIP_OK(ix->filt.codes.alloc((size_t)ix->nrows * ix->filt.stride));
   HIP_OK(ix->filt.st.alloc(8));
   HIP_OK(ix->filt.params.alloc(8));
-  HIP_OK(launch_filter_build(ix->rows.p, ix->row_bytes, ix->nrows, ix->dp, ix->filt.codes.p, ix->filt.st.p,
+  HIP_OK(launch_filter_build(ix->rows.p, ix->row_bytes, ix->nrows, ix->dp, ix->filt.stride, ix->filt.codes.p, ix->filt.st.p,
                              ix->filt.params.p, ix->stream));
   HIP_OK(hipStreamSynchronize(ix->stream));
   ix->filt.version = ix->rows_version;
@@ -450,9 +453,11 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     // Long rows (C3: 3,840 B) dwarf the 128-B probe and their searches
     // saturate any LDS-sized filter: epochs alone there.
     a.ht_log2 = 0;
+    // 512 unchecked keys in LDS (exact HBM spill beyond): C3's long rows then
+    // fit 16 waves per CU instead of 11 (+6 % QPS)
+    a.cq_cap = 512;
     if (ix->row_bytes <= 1024) {
       a.vf_log2 = 15;
-      a.cq_cap = 512;
       // -2: the filter and epochs hold accepted ids only (a few thousand per
       // query instead of ~7e4), so the filter stays sparse and almost no
       // neighbour costs an HBM probe or a mark store; rejected neighbours met
@@ -496,6 +501,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     if (shape && want) {
       if (ensure_filter(ix)) return -1;
       a.fcodes = ix->filt.codes.p;
+      a.fstride = ix->filt.stride;
       a.fparams = ix->filt.params.p;
     }
     c->launch_filtered = a.fcodes != nullptr;

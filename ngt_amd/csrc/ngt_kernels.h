@@ -73,7 +73,8 @@ struct SearchArgs {
   uint32_t cq_cap;               // unchecked LDS capacity
   uint32_t vf_log2;              // LDS visited-filter bits (log2) before the HBM epochs; 0 = none
   uint32_t accepted_only;        // epochs/filter hold only ids that entered the unchecked set
-  const uint8_t* fcodes;         // 1-byte filter copy [nrows][dp] (filter_kernels.hip) or null
+  const uint8_t* fcodes;         // 1-byte filter copy [nrows][fstride] (filter_kernels.hip) or null
+  uint64_t fstride;              // bytes per code row: dp (L2 rows of 96/128), dp rounded up to 128 B (long rows)
   const float* fparams;          // {a, b, E, X, valid} of the filter copy
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;              // [nq][k]
@@ -400,7 +401,8 @@ struct IvfSearchArgs {
 size_t ivf_search_lds_bytes(const IvfSearchArgs& a);
 // 1-byte filter copy of an L2 float repository: codes [nrows][dp], st [5]
 // scratch, params [5] = {a, b, E, X, valid}
-hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint8_t* codes,
+hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint64_t stride,
+                               uint8_t* codes,
                                uint32_t* st, float* params, hipStream_t s);
 hipError_t launch_ivf_search(const IvfSearchArgs& a, hipStream_t s);
 

@@ -510,7 +510,8 @@ __device__ __forceinline__ float cos_filter_bound(uint32_t sc, uint32_t scc, uin
 }
 
 template <int M>
-__device__ __forceinline__ void filter_cos_u8(const uint8_t* qb, const uint8_t* codes, int dp, const uint32_t* ids,
+__device__ __forceinline__ void filter_cos_u8(const uint8_t* qb, const uint8_t* codes, uint64_t stride, int dp,
+                                              const uint32_t* ids,
                                               float* out, int m, float fa, float fb, float fe,
                                               const CosFilterQuery& fq) {
   const int lane = lane_id();
@@ -519,8 +520,8 @@ __device__ __forceinline__ void filter_cos_u8(const uint8_t* qb, const uint8_t* 
   const uint32_t* qw = reinterpret_cast<const uint32_t*>(qb);
   for (int r0 = 0; r0 < m; r0 += 8) {
     const int ra = r0 + rs, rb = r0 + 4 + rs;
-    const uint32_t* xa = reinterpret_cast<const uint32_t*>(codes + (uint64_t)(ra < m ? ids[ra] : 0u) * dp);
-    const uint32_t* xb = reinterpret_cast<const uint32_t*>(codes + (uint64_t)(rb < m ? ids[rb] : 0u) * dp);
+    const uint32_t* xa = reinterpret_cast<const uint32_t*>(codes + (uint64_t)(ra < m ? ids[ra] : 0u) * stride);
+    const uint32_t* xb = reinterpret_cast<const uint32_t*>(codes + (uint64_t)(rb < m ? ids[rb] : 0u) * stride);
     uint32_t sca = 0u, scca = 0u, sqca = 0u, scb = 0u, sccb = 0u, sqcb = 0u;
     // blocks of 16 dwords per lane: every load of both rows issued before
     // the first dot product (Dp = 960: one block, one round trip)

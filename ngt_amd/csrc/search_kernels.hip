@@ -575,7 +575,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         }
         if constexpr (kFilterCos) {
           if (use_filter && m != 0) {
-            filter_cos_u8<M>(qb, a.fcodes, a.dp, st.nid, st.nd, (int)m, fa, fb, fe, fcq);
+            filter_cos_u8<M>(qb, a.fcodes, a.fstride, a.dp, st.nid, st.nd, (int)m, fa, fb, fe, fcq);
             __syncthreads();
             const bool keep = (uint32_t)lane < m && !(st.nd[lane] > expr);
             const uint32_t myid = (uint32_t)lane < m ? st.nid[lane] : 0u;
