@@ -258,6 +258,30 @@ int ngt_amd_merge_packed_device(int device, const uint64_t *d_packed, uint32_t n
                                 uint32_t k, const uint32_t *id_offsets, uint32_t *d_out_ids,
                                 float *d_out_dists, uint32_t *d_out_n, void *stream);
 
+/* ---- sharded repository over the GPUs of a node (shard_api.cpp) --------- *
+ * SURVEY.md 8(e), BASELINE C4/C5: rank r holds shard r (global ids
+ * id_offsets[r] + 1 ..) as its own index; each call searches the batch on the
+ * shard, packs the per-query top-k, exchanges them with ONE RCCL all-gather
+ * (nq * k * 8 B per rank) and merges on the device, so every rank returns the
+ * k best over the union by (distance, global id) (Common.h:1937-1992).
+ * ngt_amd_shard_unique_id fills an RCCL unique id (>= 128 bytes) on one rank;
+ * the caller distributes it and every rank creates its communicator with it.
+ * id_offsets: host array of every rank's offset.  One call at a time per
+ * communicator.  Replaces nothing in the reference (NGT has no multi-GPU
+ * form); the per-shard searches replace NGT::Index::search /
+ * NGTQG::Index::search. */
+typedef struct ngt_amd_shard_comm ngt_amd_shard_comm;
+int ngt_amd_shard_unique_id(uint8_t *id, uint64_t id_bytes);
+int ngt_amd_shard_comm_create(ngt_amd_shard_comm **comm, int device, int rank, int world,
+                              const uint8_t *id, uint64_t id_bytes);
+int ngt_amd_shard_comm_destroy(ngt_amd_shard_comm *comm);
+int ngt_amd_sharded_search_device(ngt_amd_shard_comm *comm, ngt_amd_index *index,
+                                  const ngt_amd_search_params *params, const void *d_queries,
+                                  uint64_t query_bytes, uint32_t nq, const uint32_t *d_seeds,
+                                  const uint64_t *d_seed_off, const uint32_t *id_offsets,
+                                  uint32_t *d_out_ids, float *d_out_dists, uint32_t *d_out_n,
+                                  void *stream);
+
 /* ---- NGTQG quantized graph (L2, float objects) -------------------------- *
  *   ngt_amd_qg_set_quantizer  <- the NGTQ::Quantizer NGTQG::Index opens from
  *                                <index>/qg (lib/NGT/NGTQ/QuantizedGraph.h:170-185):
@@ -339,6 +363,14 @@ int ngt_amd_qg_search_device(ngt_amd_index *index, const ngt_amd_qg_search_param
                              const void *d_queries, uint64_t query_bytes, uint32_t nq,
                              const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,
                              float *d_dists, uint32_t *d_n, uint64_t *d_counters, void *stream);
+
+/* NGTQG form of the sharded search (BASELINE C5): as ngt_amd_sharded_search_device. */
+int ngt_amd_sharded_qg_search_device(ngt_amd_shard_comm *comm, ngt_amd_index *index,
+                                     const ngt_amd_qg_search_params *params, const void *d_queries,
+                                     uint64_t query_bytes, uint32_t nq, const uint32_t *d_seeds,
+                                     const uint64_t *d_seed_off, const uint32_t *id_offsets,
+                                     uint32_t *d_out_ids, float *d_out_dists, uint32_t *d_out_n,
+                                     void *stream);
 
 /* ---- NGTQ IVF-ADC ------------------------------------------------------- *
  *   ngt_amd_ngtq_open          <- NGTQ::Index(path) (lib/NGT/NGTQ/Quantizer.h:2832-2836,

@@ -88,6 +88,12 @@ def declare(L):
                                                  vp]),
         "ngt_amd_pack_results_device": (c_int, [c_int, vp, vp, vp, c_uint32, c_uint32, vp, vp]),
         "ngt_amd_merge_packed_device": (c_int, [c_int, vp, c_uint32, c_uint32, c_uint32, vp, vp, vp, vp, vp]),
+        "ngt_amd_shard_unique_id": (c_int, [vp, c_uint64]),
+        "ngt_amd_shard_comm_create": (c_int, [vp, c_int, c_int, c_int, vp, c_uint64]),
+        "ngt_amd_shard_comm_destroy": (c_int, [vp]),
+        "ngt_amd_sharded_search_device": (c_int, [vp, vp, vp, vp, c_uint64, c_uint32, vp, vp, vp, vp, vp, vp, vp]),
+        "ngt_amd_sharded_qg_search_device": (c_int, [vp, vp, vp, vp, c_uint64, c_uint32, vp, vp, vp, vp, vp, vp,
+                                                     vp]),
         "ngt_amd_qg_set_quantizer": (c_int, [vp, vp, vp, c_uint32, c_uint32]),
         "ngt_amd_qg_build_graph": (c_int, [vp, vp, c_uint32]),
         "ngt_amd_qg_encode": (c_int, [vp, vp]),

@@ -155,3 +155,50 @@ class ShardedIndex(object):
                                     d_seeds=seeds, d_seed_off=seed_off, stream=stream,
                                     visited_hash_log2=visited_hash_log2)
         return self.merge_local(ids, ds, n, k, stream)
+
+
+class RcclShardComm(object):
+    """The C ABI's sharded search (shard_api.cpp) for callers without
+    torch.distributed: an RCCL communicator of one rank per GPU, and one call
+    that searches the batch on this rank's shard, all-gathers the packed
+    per-shard top-k and merges them on the device."""
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        import ctypes
+        L = lib()
+        buf = (ctypes.c_uint8 * RcclShardComm.ID_BYTES)()
+        if L.ngt_amd_shard_unique_id(buf, RcclShardComm.ID_BYTES) != 0:
+            raise NativeError(L.ngt_amd_last_error().decode())
+        return bytes(buf)
+
+    def __init__(self, device, rank, world, uid):
+        import ctypes
+        self.L = lib()
+        self.world = world
+        self.h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * len(uid)).from_buffer_copy(uid)
+        if self.L.ngt_amd_shard_comm_create(ctypes.byref(self.h), device, rank, world, buf, len(uid)) != 0:
+            raise NativeError(self.L.ngt_amd_last_error().decode())
+
+    def search_device(self, index, d_queries, query_bytes, nq, offsets, d_ids, d_dists, d_n, k=10, epsilon=0.1,
+                      radius=-1.0, edge_size=-1, seed_mode=0, d_seeds=None, d_seed_off=None, stream=None,
+                      visited_hash_log2=0, qg=False, result_expansion=3.0):
+        import ctypes
+        from ._sigs import QgSearchParams, SearchParams
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        if qg:
+            prm = QgSearchParams(k, epsilon, result_expansion, radius, seed_mode, visited_hash_log2)
+            fn = self.L.ngt_amd_sharded_qg_search_device
+        else:
+            prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, visited_hash_log2, 0)
+            fn = self.L.ngt_amd_sharded_search_device
+        if fn(self.h, index.h, ctypes.byref(prm), d_queries, query_bytes, nq, d_seeds, d_seed_off, off.ctypes.data,
+              d_ids, d_dists, d_n, stream) != 0:
+            raise NativeError(self.L.ngt_amd_last_error().decode())
+
+    def close(self):
+        if self.h:
+            self.L.ngt_amd_shard_comm_destroy(self.h)
+            self.h = None

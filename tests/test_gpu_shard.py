@@ -167,3 +167,70 @@ def test_sharded_index_one_rank_nccl():
         qix.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_sharded_search_c_abi():
+    """The C ABI's sharded search (ngt_amd_sharded_search_device /
+    _qg_search_device: per-shard search, pack, one RCCL all-gather, device
+    merge) on a one-rank communicator: exact search against the oracle with a
+    global id offset, NGTQG search against the reference's C1 results."""
+    import torch
+    from ngt_amd.device import SEED_GIVEN, SEED_TREE, DeviceIndex
+    from ngt_amd.shard import RcclShardComm
+    from test_gpu_parity import _random_graph
+    dev = torch.device("cuda:0")
+    comm = RcclShardComm(0, 0, 1, RcclShardComm.unique_id())
+    try:
+        n, dim, deg, nq, k, off = 4000, 32, 16, 64, 10, 1000
+        rows, offs, edges = _random_graph(n, dim, deg, 11)
+        ix = DeviceIndex("l2", "float", dim)
+        ix.set_objects(rows)
+        ix.set_graph(offs, edges)
+        rng = np.random.default_rng(5)
+        qs = rng.random((nq, dim), dtype=np.float32)
+        seeds = np.stack([rng.choice(np.arange(1, n), 8, replace=False) for _ in range(nq)]).astype(np.uint32)
+        d_q = torch.from_numpy(qs).to(dev)
+        d_s = torch.from_numpy(seeds.reshape(-1).view(np.int32)).to(dev)
+        d_o = torch.arange(0, nq + 1, dtype=torch.int64, device=dev) * 8
+        oi = torch.zeros((nq, k), dtype=torch.int32, device=dev)
+        od = torch.zeros((nq, k), dtype=torch.float32, device=dev)
+        on = torch.zeros((nq,), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        comm.search_device(ix, d_q.data_ptr(), dim * 4, nq, [off], oi.data_ptr(), od.data_ptr(), on.data_ptr(), k=k,
+                           epsilon=0.2, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_s.data_ptr(),
+                           d_seed_off=d_o.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        gi, gd, gn = oi.cpu().numpy().view(np.uint32), od.cpu().numpy(), on.cpu().numpy()
+        for i in range(nq):
+            oid, odist, _ = O.search("l2", rows, offs, edges, qs[i], seeds[i], k, np.float32(0.2))
+            assert list(gi[i, :gn[i]]) == list(oid + off), i
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), odist.view(np.uint32))
+        ix.close()
+
+        from test_gpu_qg import device_qg, state
+        _, _, _, _, _, _, _, z, meta, dim, _ = state("c1_qg")
+        qix = device_qg("c1_qg")
+        qsq = z["queries"].astype(np.float32)
+        d_q = torch.from_numpy(qsq).to(dev)
+        for key in ("10_0.05_3", "20_0.03_3"):
+            k, eps, exp = key.split("_")
+            k = int(k)
+            oi = torch.zeros((len(qsq), k), dtype=torch.int32, device=dev)
+            od = torch.zeros((len(qsq), k), dtype=torch.float32, device=dev)
+            on = torch.zeros((len(qsq),), dtype=torch.int32, device=dev)
+            comm.search_device(qix, d_q.data_ptr(), dim * 4, len(qsq), [0], oi.data_ptr(), od.data_ptr(),
+                               on.data_ptr(), k=k, epsilon=float(eps), seed_mode=SEED_TREE, stream=stream, qg=True,
+                               result_expansion=float(exp))
+            torch.cuda.synchronize()
+            gi, gd, gn = oi.cpu().numpy().view(np.uint32), od.cpu().numpy(), on.cpu().numpy()
+            for qi in range(len(qsq)):
+                n = int(z["n_" + key][qi])
+                ref_ids = z["ids_" + key][qi][:n]
+                valid = ref_ids != 0
+                assert int(gn[qi]) == int(valid.sum()), (key, qi)
+                assert list(gi[qi, :gn[qi]]) == list(ref_ids[valid]), (key, qi)
+                assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32),
+                                      z["dist_" + key][qi][:n][valid].view(np.uint32)), (key, qi)
+        qix.close()
+    finally:
+        comm.close()
