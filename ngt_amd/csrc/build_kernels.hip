@@ -21,6 +21,64 @@
 
 namespace ngt_amd {
 
+// Node.cpp:117-129 as the reference's -Ofast build (GCC, AVX2) evaluates it
+// (read from its object code): the sums over a row of the distance matrix
+// run in four double lanes, lane l adding x[8b + l] + x[8b + l + 4] per block
+// of 8, folded (l1 + l3) + (l0 + l2); then one 4-element block
+// ((y1 + y3) + (y0 + y2)) if at least 4 remain, then the rest one by one;
+// pow(d, 2) is d * d contracted into FMAs (lane l: fma(lo, lo, hi * hi)), and
+// both divisions by fsize are multiplies by its reciprocal.  The order matters
+// when variances tie in real arithmetic (duplicate-heavy or symmetric data).
+__device__ inline double pivot_variance(const float* x, uint32_t n) {
+  const double inv = 1.0 / (double)n;
+  const uint32_t n8 = n & ~7u;
+  double s = 0.0;
+  uint32_t j = 0;
+  if (n > 7) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (uint32_t b = 0; b < n8; b += 8) {
+      a0 += (double)x[b] + (double)x[b + 4];
+      a1 += (double)x[b + 1] + (double)x[b + 5];
+      a2 += (double)x[b + 2] + (double)x[b + 6];
+      a3 += (double)x[b + 3] + (double)x[b + 7];
+    }
+    s = (a1 + a3) + (a0 + a2);
+    j = n8;
+    if (n - n8 >= 4) {
+      s += ((double)x[j + 1] + (double)x[j + 3]) + ((double)x[j] + (double)x[j + 2]);
+      j += 4;
+    }
+  }
+  for (; j < n; j++) s += (double)x[j];
+  const double avg = s * inv;
+  double v = 0.0;
+  j = 0;
+  if (n > 7) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (uint32_t b = 0; b < n8; b += 8) {
+      double lo, hi;
+      lo = (double)x[b] - avg; hi = (double)x[b + 4] - avg; a0 += fma(lo, lo, hi * hi);
+      lo = (double)x[b + 1] - avg; hi = (double)x[b + 5] - avg; a1 += fma(lo, lo, hi * hi);
+      lo = (double)x[b + 2] - avg; hi = (double)x[b + 6] - avg; a2 += fma(lo, lo, hi * hi);
+      lo = (double)x[b + 3] - avg; hi = (double)x[b + 7] - avg; a3 += fma(lo, lo, hi * hi);
+    }
+    v = (a1 + a3) + (a0 + a2);
+    j = n8;
+    if (n - n8 >= 4) {
+      const double y0 = (double)x[j] - avg, y1 = (double)x[j + 1] - avg;
+      const double y2 = (double)x[j + 2] - avg, y3 = (double)x[j + 3] - avg;
+      v += fma(y1, y1, y3 * y3) + fma(y0, y0, y2 * y2);
+      j += 4;
+    }
+  }
+  for (; j < n; j++) {
+    const double d = (double)x[j] - avg;
+    v = fma(d, d, v);
+  }
+  return v * inv;
+}
+
+
 namespace {
 
 constexpr uint32_t kLeaf = 0x80000000u;
@@ -340,17 +398,7 @@ __global__ void __launch_bounds__(256) ngt_tree_insert_kernel(TreeBuildArgs a) {
     }
     for (uint32_t i = tid; i < fsize; i += 256) D[i * fsize + i] = 0.f;
     __syncthreads();
-    for (uint32_t i = tid; i < fsize; i += 256) {
-      double avg = 0.0;
-      for (uint32_t j = 0; j < fsize; j++) avg += (double)D[i * fsize + j];
-      avg /= (double)fsize;
-      double v = 0.0;
-      for (uint32_t j = 0; j < fsize; j++) {
-        const double x = (double)D[i * fsize + j] - avg;
-        v += x * x;  // pow(x, 2.0)
-      }
-      var[i] = v / (double)fsize;
-    }
+    for (uint32_t i = tid; i < fsize; i += 256) var[i] = pivot_variance(D + (uint64_t)i * fsize, fsize);
     __syncthreads();
     uint32_t pv = 0;
     {

@@ -23,6 +23,7 @@
 #include "../../include/ngt_amd.h"
 #include "coalesce.h"
 #include "index_io.h"
+#include "kmeans_ngt.h"
 
 namespace {
 
@@ -233,6 +234,75 @@ void ngtqg_close_index(NGTQGIndex index) {
   delete static_cast<QgCapiIndex*>(index);
 }
 
+// The local codebooks of NGTQG::Index::quantize: NGTQ's dynamic k-means
+// (Quantizer.h:1802-1858) inserts the residuals (object - global centroid, the
+// zero vector for a quantized graph, QuantizedGraph.h:396-400) of the first
+// localCentroidLimit x localClusteringSampleCoefficient = 16 x 100 objects
+// into each local codebook index (ANNG, edge sizes 10/40, batch 200,
+// insertion coefficient 1.1: the local prf the reference writes), then runs
+// NGT::Clustering::kmeansWithNGT on it (kmeans_ngt.h).  Here each sample
+// index is built by this library's device construction (ngt_create_index)
+// and every assignment search is a device graph search (ngt_batch_search_index,
+// tree seeds); the clustering logic is the restatement in kmeans_ngt.h.  The
+// reference parallelises those searches with OpenMP while its tree-seed
+// thinning draws from the process-wide rand() (Index.h:1555-1559), so its own
+// codebooks differ from run to run; run with one OpenMP thread it is
+// deterministic, and that is what this reproduces (tests/golden/c1_qg_st).
+static std::string train_local_kmeans_ngt(const ngt_amd::HostIndex& h, uint32_t M, uint32_t dsub,
+                                          std::vector<float>& local) {
+  std::vector<uint64_t> sample;
+  for (uint64_t i = 1; i < h.nrows && sample.size() < 16 * 100; i++)
+    if (h.valid[i]) sample.push_back(i);
+  const uint32_t n = (uint32_t)sample.size();
+  local.assign((size_t)M * 16 * dsub, 0.0f);
+  for (uint32_t m = 0; m < M; m++) {
+    std::vector<std::vector<float>> vectors(n, std::vector<float>(dsub));
+    std::vector<float> flat((size_t)n * dsub);
+    for (uint32_t i = 0; i < n; i++) {
+      const float* r = reinterpret_cast<const float*>(h.rows.data() + sample[i] * h.row_bytes);
+      for (uint32_t j = 0; j < dsub; j++) vectors[i][j] = flat[(size_t)i * dsub + j] = r[(size_t)m * dsub + j];
+    }
+    NGTError err = ngt_create_error_object();
+    NGTProperty prop = ngt_create_property(err);
+    std::string e;
+    NGTIndex idx = nullptr;
+    if (!prop || !ngt_set_property_dimension(prop, (int32_t)dsub, err) ||
+        !ngt_set_property_edge_size_for_creation(prop, 10, err) ||
+        !ngt_set_property_edge_size_for_search(prop, 40, err) || !ngt_set_property_object_type_float(prop, err) ||
+        !ngt_set_property_distance_type_l2(prop, err) || !(idx = ngt_create_graph_and_tree_in_memory(prop, err)) ||
+        !ngt_batch_append_index(idx, flat.data(), n, err) || !ngt_create_index(idx, 24, err))
+      e = ngt_get_error_string(err);
+    if (e.empty()) {
+      ngt_amd::kmeans::SearchFn search = [&](const std::vector<std::vector<float>>& qs, size_t size, float eps,
+                                             std::vector<std::vector<std::pair<uint32_t, float>>>& out) {
+        const uint32_t nq = (uint32_t)qs.size();
+        std::vector<float> q((size_t)nq * dsub);
+        for (uint32_t i = 0; i < nq; i++) std::copy(qs[i].begin(), qs[i].end(), q.begin() + (size_t)i * dsub);
+        std::vector<uint32_t> ids((size_t)nq * size), cnt(nq);
+        std::vector<float> ds((size_t)nq * size);
+        if (!ngt_batch_search_index(idx, q.data(), nq, (int32_t)dsub, size, eps, -1.0f, -1, ids.data(), ds.data(),
+                                    cnt.data(), err))
+          return false;
+        out.assign(nq, {});
+        for (uint32_t i = 0; i < nq; i++)
+          for (uint32_t r = 0; r < cnt[i]; r++) out[i].push_back({ids[(size_t)i * size + r], ds[(size_t)i * size + r]});
+        return true;
+      };
+      std::vector<std::vector<float>> cents;
+      ngt_amd::kmeans::Params prm;
+      if (ngt_amd::kmeans::kmeans_with_ngt(search, vectors, 16, prm, cents, e) < 0.0 && e == "search failed")
+        e = ngt_get_error_string(err);
+      for (size_t c = 0; c < cents.size() && c < 16; c++)
+        for (uint32_t j = 0; j < dsub; j++) local[((size_t)m * 16 + c) * dsub + j] = cents[c][j];
+    }
+    if (idx) ngt_close_index(idx);
+    if (prop) ngt_destroy_property(prop);
+    ngt_destroy_error_object(err);
+    if (!e.empty()) return "local codebook " + std::to_string(m) + ": " + e;
+  }
+  return "";
+}
+
 // NGTQG::Index::quantize (lib/NGT/NGTQ/QuantizedGraph.h:456-475) on the device:
 // nothing when <index>/qg exists; else the quantizer frame (:423-454), the
 // codebooks, every object's local codes (:392-421) and the quantized graph
@@ -240,7 +310,7 @@ void ngtqg_close_index(NGTQGIndex index) {
 // qg/global and qg/local-<m> as NGT indexes (built by this library's ANNG
 // construction), qg/ivt (Repository<InvertedIndexEntry<uint16_t>>) and qg/grp
 // (QuantizedGraphRepository::serialize, :117-128).  The local codebooks come
-// from ngt_amd_qg_train (Lloyd), not the reference's kmeansWithNGT.
+// from the kmeansWithNGT restatement above (train_local_kmeans_ngt).
 bool ngtqg_quantize(const char* indexPath, NGTQGQuantizationParameters parameters, NGTError error) {
   auto err = [&](const std::string& e) {
     report(error, std::string("Capi : ") + __FUNCTION__ + "() : Error: " + e);
@@ -273,10 +343,14 @@ bool ngtqg_quantize(const char* indexPath, NGTQGQuantizationParameters parameter
   if (const char* env = getenv("NGT_AMD_DEVICE")) dev = atoi(env);
   if (ngt_amd_index_create(&ix.dev, dev, h.prop.distance_type, h.prop.object_type, dim)) return err(amd_err());
   if (ngt_amd_index_set_objects(ix.dev, h.rows.data(), h.nrows, h.valid.data())) return err(amd_err());
-  // the dynamic k-means samples the first localCentroidLimit * LocalSampleCoefficient objects
-  const uint32_t nsample = (uint32_t)std::min<uint64_t>(16 * 100, h.nrows - 1);
-  std::vector<float> local((size_t)M * 16 * dsub);
-  if (ngt_amd_qg_train(ix.dev, M, nsample, 20, local.data(), nullptr)) return err(amd_err());
+  std::vector<float> local;
+  e = train_local_kmeans_ngt(h, M, (uint32_t)dsub, local);
+  if (!e.empty()) return err(e);
+  {
+    // the encoder below takes the codebooks from the device quantizer
+    std::vector<float> zero(dim, 0.0f);
+    if (ngt_amd_qg_set_quantizer(ix.dev, zero.data(), local.data(), M, (uint32_t)dsub)) return err(amd_err());
+  }
   std::vector<uint8_t> codes((size_t)h.nrows * M);
   if (ngt_amd_qg_encode(ix.dev, codes.data())) return err(amd_err());
   const uint32_t max_edges = (uint32_t)parameters.max_number_of_edges;

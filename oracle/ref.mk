@@ -57,3 +57,6 @@ $(OUT)/ngtq: $(REF)/bin/ngtq/ngtq.cpp $(OUT)/libngt_ref.so
 
 $(OUT)/ngtq_harness: tests/golden/ngtq_harness.cpp $(OUT)/libngt_ref.so
 	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lngt_ref -Wl,-rpath,$(abspath $(OUT))
+
+$(OUT)/kmeans_harness: tests/golden/kmeans_harness.cpp ngt_amd/csrc/kmeans_ngt.h $(OUT)/libngt_ref.so
+	$(CXX) $(CXXFLAGS) -Ingt_amd/csrc -o $@ $< -L$(OUT) -lngt_ref -Wl,-rpath,$(abspath $(OUT))

@@ -317,6 +317,10 @@ def test_ngtqg_quantize_capi(tmp_path):
     for sub in ["global", "local-0", "local-127"]:
         assert sorted(os.listdir(os.path.join(q, sub))) == ["grp", "obj", "prf", "tre"], sub
     mine = F.read_qg(str(d), offs, ids, 128)
+    # the codebooks: kmeansWithNGT restated over device searches, equal to the
+    # reference's own quantize run with one OpenMP thread (make_kmeans_goldens.py)
+    st = np.load(os.path.join(GOLD, "qg_kmeans_st.npz"))["c1"]
+    assert np.array_equal(mine["local"][:, 1:17, 0].view(np.uint32), st.view(np.uint32))
     # the codes in ivt are the encoder's for the written codebooks
     ix = DeviceIndex("l2", "float", dim)
     ix.set_objects(rows, valid)
@@ -410,3 +414,18 @@ def test_qg_wide_subspace_counts_exact(dim):
             assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32)), (dim, k, qi)
             assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt], (dim, k, qi)
     ix.close()
+
+
+def test_ngtqg_quantize_codebooks_dsub4(tmp_path):
+    """ngtqg_quantize -Q 4 on the 20-d index: the 5 local codebooks (16
+    centroids of 4 floats) equal the reference's single-thread quantize."""
+    from ngt_amd.qg import quantize
+    d = tmp_path / "d20"
+    d.mkdir()
+    for f in ["prf", "obj", "grp", "tre"]:
+        os.symlink(os.path.join(GOLD, "d20_qg", f), str(d / f))
+    quantize(str(d), 4, 64)
+    st = np.load(os.path.join(GOLD, "qg_kmeans_st.npz"))["d20"]
+    for m in range(5):
+        rows, _ = F.read_obj(os.path.join(str(d), "qg", "local-%d" % m, "obj"), 4, np.float32)
+        assert np.array_equal(rows[1:17, :4].view(np.uint32), st[m].view(np.uint32)), m
