@@ -80,6 +80,9 @@ def main():
         ch = harness(rows, M, dsub, work)
         assert np.array_equal(ca.view(np.uint32), ch.view(np.uint32)), "restatement differs: " + tag
         res[tag] = ca.reshape(M, 16) if dsub == 1 else ca
+        import hashlib
+        for f in ("ivt", "grp"):
+            print(tag, "qg/%s sha256" % f, hashlib.sha256(open(os.path.join(a, "qg", f), "rb").read()).hexdigest())
         print(tag, "M", M, "dsub", dsub, ": two single-thread reference runs and the restatement agree")
     np.savez(os.path.join(HERE, "qg_kmeans_st.npz"), **res)
     shutil.rmtree(work, ignore_errors=True)

@@ -321,6 +321,11 @@ def test_ngtqg_quantize_capi(tmp_path):
     # reference's own quantize run with one OpenMP thread (make_kmeans_goldens.py)
     st = np.load(os.path.join(GOLD, "qg_kmeans_st.npz"))["c1"]
     assert np.array_equal(mine["local"][:, 1:17, 0].view(np.uint32), st.view(np.uint32))
+    # with those codebooks, qg/ivt and qg/grp are the single-thread reference's bytes
+    sha = {f: hashlib.sha256(open(os.path.join(q, f), "rb").read()).hexdigest() for f in ("ivt", "grp")}
+    print("ngtqg_quantize sha256", sha)
+    assert sha["ivt"] == "f4a5c511c370ed63c8f626db456c181558e43b2754ae10e8ebc79c865a97b0db"
+    assert sha["grp"] == "45bfcbbe1adc1bda34a1430d545751e538db6b7e0f838afdfe6e594a5e8ef527"
     # the codes in ivt are the encoder's for the written codebooks
     ix = DeviceIndex("l2", "float", dim)
     ix.set_objects(rows, valid)
