@@ -192,7 +192,10 @@ struct Params {
   float epsilon_from = 0.10f, epsilon_to = 0.50f, epsilon_step = 0.05f;  // Quantizer.h:1848-1850
   size_t maximum_iteration = 20;                                        // :1851
   size_t result_size_coefficient = 5;                                   // Clustering.h:102
-  bool cluster_size_constraint = false;                                 // uninitialised in the reference
+  // Clustering::clusterSizeConstraint is never initialised by the constructor
+  // NGTQ uses; the reference's build behaves as false (pinned by the
+  // single-thread fixtures, tests/golden/qg_kmeans_st.npz)
+  bool cluster_size_constraint = false;
 };
 
 // kmeansWithNGT(index, numberOfClusters, clusters) (Clustering.h:724-742):
