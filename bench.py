@@ -173,15 +173,28 @@ def recall_at(ids, gt, k):
     return hit / float(gt.shape[0] * k)
 
 
-def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.0005):
+# the epsilon sweep stops doubling once one launch takes this long (the sweep
+# is setup, not the measurement; a multi-second launch means the graph needs
+# an epsilon that no serving configuration would use)
+SWEEP_KERNEL_MS_CAP = float(os.environ.get("NGT_BENCH_SWEEP_MS_CAP", "3000"))
+
+
+def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.0005, last_ms=None):
     """Smallest epsilon whose mean recall@k reaches the target (ngt eval
-    semantics, Optimizer.h:400): given candidates, or by doubling + bisection."""
+    semantics, Optimizer.h:400): given candidates, or by doubling + bisection.
+    last_ms() = the kernel time of the latest measurement: the doubling stops
+    at SWEEP_KERNEL_MS_CAP (the result is then the last epsilon tried, whose
+    recall the line reports)."""
     if eps_list:
         for eps in eps_list:
             if measure(eps) >= target:
                 return eps
         return eps_list[-1]
     while measure(hi) < target and hi < 4.0:
+        if last_ms is not None and last_ms() > SWEEP_KERNEL_MS_CAP:
+            log("eps sweep: %.1f ms per launch at eps %.4f exceeds the %.0f ms cap; stopping" % (
+                last_ms(), hi, SWEEP_KERNEL_MS_CAP))
+            return hi
         lo, hi = hi, hi * 2
     while hi - lo > tol:
         mid = 0.5 * (lo + hi)
@@ -210,6 +223,13 @@ def main():
                     help="knn: exact kNN graph built in setup (out/in edges); anng: this library's own "
                          "ngt_create_index ANNG (GraphAndTreeIndex::createIndex on the device)")
     ap.add_argument("--anng-edges", type=int, default=10, help="--graph anng: edgeSizeForCreation (ngt create -E)")
+    ap.add_argument("--edge-size", type=int, default=None,
+                    help="sc.edgeSize of the searches (getEdgeSize, Graph.h:675-692): -1 = the index's "
+                         "EdgeSizeForSearch (an `ngt create` index: 40), 0 = every edge; default -1 for "
+                         "--graph anng, 0 for the kNN graph")
+    ap.add_argument("--seeds", choices=["random", "tree"], default=None,
+                    help="random: getRandomSeeds (graph-only search); tree: the DVP tree's leaf "
+                         "(GraphAndTreeIndex::search, `ngt search`'s default); default tree for --graph anng")
     ap.add_argument("--knn", type=int, default=128)
     ap.add_argument("--out-deg", type=int, default=48)
     ap.add_argument("--in-deg", type=int, default=96)
@@ -230,6 +250,11 @@ def main():
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
     qgm = args.mode == "qg" or (args.mode == "shard" and args.qg)
+    if args.edge_size is None:
+        args.edge_size = -1 if args.graph == "anng" else 0
+    if args.seeds is None:
+        args.seeds = "tree" if args.graph == "anng" and not qgm else "random"
+    es_prop = 40 if args.graph == "anng" else 0  # the prf's EdgeSizeForSearch (Command.cpp:40)
     if qgm and args.visited == -2:
         args.visited = -1  # the QG search marks accepted ids only by definition (QuantizedGraph.h:241-266)
     c3 = args.config == "c3"
@@ -278,12 +303,13 @@ def main():
     ix = DeviceIndex(metric, "float", D, device=local)
     ix.set_objects_device(rows.data_ptr(), N + 1)
     build_s = None
+    tree = None
     if args.graph == "anng":
         # the index a user of `ngt create -g a -E <e>` gets, built by this
         # library's own device construction (byte-identical to the
         # reference's at C1, tests/test_gpu_build.py)
         t0 = time.time()
-        (h_off, h_ids, _), _tree = ix.build_anng(edge_size_for_creation=args.anng_edges)
+        (h_off, h_ids, _), tree = ix.build_anng(edge_size_for_creation=args.anng_edges, edge_size_for_search=es_prop)
         build_s = time.time() - t0
         offsets = torch.from_numpy(h_off.astype(np.int64)).to(dev)
         edges = torch.from_numpy(h_ids.astype(np.int32)).to(dev)
@@ -292,8 +318,11 @@ def main():
     else:
         offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev,
                                      cosine=c3)
+    ix.set_search_property(es_prop, 30, 20, args.seed_size, 0)
     ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
-    ix.set_search_property(0, 30, 20, args.seed_size, 0)
+    if tree is not None:
+        ix.set_tree(tree)
+    es_resolved = int(ix.resolve_edge_size(args.edge_size, 0.1))
     stream = torch.cuda.current_stream(dev).cuda_stream
     # queries prepared on the device like Index::allocateObject (pad; normalize
     # for the normalized metrics)
@@ -337,9 +366,16 @@ def main():
                 "mfma_bf16_frac": 2.0 * macs / (ms * 1e-3) / 2.5e15}
         log("exact scan: %.2f ms per %d queries (%.0f QPS)" % (ms, NQ, scan["qps"]))
 
-    seeds = random_seeds(N + 1, NQ, args.seed_size)
-    d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
-    d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * args.seed_size
+    if args.seeds == "tree":
+        if tree is None:
+            raise SystemExit("bench: --seeds tree needs an index with a DVP tree (--graph anng)")
+        # GraphAndTreeIndex::getSeedsFromTree on the device, once (the seed
+        # lists are the search's input, like the random ones below)
+        seeds, d_seeds, d_soff = tree_seed_lists(ix, qdev, dp, NQ, K, dev, torch)
+    else:
+        seeds = random_seeds(N + 1, NQ, args.seed_size)
+        d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+        d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * args.seed_size
     # consecutive steps alternate over `--streams` HIP streams (each with its
     # own output buffers and, inside the library, its own launch scratch), so
     # a step's kernel starts while the previous step's last queries drain
@@ -375,7 +411,7 @@ def main():
                 result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
             return
         ix.search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
-                         oc.data_ptr(), k=K, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN,
+                         oc.data_ptr(), k=K, epsilon=eps, edge_size=args.edge_size, seed_mode=SEED_GIVEN,
                          d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=streams[si],
                          visited_hash_log2=visited)
         if shard:
@@ -391,7 +427,8 @@ def main():
         log("eps %.4f recall@%d %.4f kernel %.2f ms" % (eps, K, r, sweep[-1][2]))
         return r
 
-    chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None)
+    chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None,
+                          last_ms=lambda: sweep[-1][2])
     rec = measure(chosen)
     if dist is not None and not shard:
         # replicas: all ranks use the largest epsilon any rank needed
@@ -491,7 +528,8 @@ def main():
         run(chosen, 0)  # the timed configuration's own results
         torch.cuda.synchronize()
         gpu_out = (out_i.cpu().numpy().view(np.uint32), out_d.cpu().numpy(), out_n.cpu().numpy().view(np.uint32))
-        cpu, parity = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric, gpu_out, full_cnt)
+        cpu, parity = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric, gpu_out, full_cnt,
+                                   es_resolved=int(ix.resolve_edge_size(args.edge_size, chosen)))
         if scan is not None:
             scan["oracle_sample"] = scan_sample_check(rows, qdev, metric, K, gt_i, gt_d, gt_n)
 
@@ -529,8 +567,14 @@ def main():
             "dtype": "f32" if not qgm else "u4-adc/u8-lut/f32-rerank",
             "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
             "config": {"workload": workload,
-                       "recall_at_10": rec, "epsilon": chosen, "edge_size": "all", "graph": graph,
-                       "seeds": "getRandomSeeds (%d)" % args.seed_size,
+                       "recall_at_10": rec, "epsilon": chosen,
+                       "edge_size": ("all" if args.edge_size == 0 else
+                                     "%d (sc.edgeSize %d; the prf's EdgeSizeForSearch %d)" % (
+                                         es_resolved, args.edge_size, es_prop)),
+                       "graph": graph,
+                       "seeds": ("getSeedsFromTree (DVP tree leaf, seed size %d)" % args.seed_size
+                                 if args.seeds == "tree" else "getRandomSeeds (%d)" % args.seed_size),
+                       "sweep_kernel_ms_cap": SWEEP_KERNEL_MS_CAP,
                        "distance_computations_per_query": float(c[:, 0].mean()),
                        "expansions_per_query": float(c[:, 2].mean()),
                        "visited_set": ("hbm-epochs, every evaluated id (accepted-only and the LDS filter are "
@@ -598,6 +642,29 @@ def measured_traffic(mode, config, graph, eps, visited, filtered=False):
                 and bool(e.get("filtered", False)) == bool(filtered)):
             return float(e["traffic_bytes"]), e
     return None, {}
+
+
+def tree_seed_lists(ix, qdev, dp, nq, k, dev, torch):
+    """Tree seeds of every query (getSeedsFromTree, Index.h:1524-1567) from
+    the device: one k-result graph search with seed_mode TREE would also
+    produce them, but the lists themselves are what the oracle leg needs, so
+    they come from ngt_amd_tree_seeds_device as [nq][<=seed stride] + counts."""
+    L = ix.L
+    stride = 128
+    d_s = torch.zeros((nq, stride), dtype=torch.int32, device=dev)
+    d_c = torch.zeros((nq,), dtype=torch.int32, device=dev)
+    rc = L.ngt_amd_tree_seeds_device(ix.h, qdev.data_ptr(), dp * 4, nq, k, d_s.data_ptr(), stride,
+                                     d_c.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    if rc != 0:
+        raise SystemExit("bench: tree seeds failed: %s" % L.ngt_amd_last_error().decode())
+    torch.cuda.synchronize()
+    cnt = d_c.cpu().numpy().astype(np.int64)
+    s = d_s.cpu().numpy().view(np.uint32)
+    seeds = [s[i, :cnt[i]].copy() for i in range(nq)]
+    off = np.zeros(nq + 1, np.int64)
+    off[1:] = np.cumsum(cnt)
+    flat = np.concatenate(seeds).astype(np.uint32)
+    return seeds, torch.from_numpy(flat.view(np.int32)).to(dev), torch.from_numpy(off).to(dev)
 
 
 def write_ngt_index(path, rows, offsets, edges, dim):
@@ -772,7 +839,7 @@ def scan_sample_check(rows, qdev, metric, k, gt_i, gt_d, gt_n, nsample=16):
     return {"queries": nsample, "identical": True}
 
 
-def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_out, gpu_cnt):
+def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_out, gpu_cnt, es_resolved=0):
     """The CPU baseline and the parity sample in one: the oracle restatement
     (oracle/ngt_oracle.c, the reference's 16-lane FMA order) built -O3 for the
     host's widest ISA (x86-64-v4 AVX-512, else v3) with one query per thread on
@@ -809,7 +876,7 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
             return O.qg_search_batch(qg, h_rows, h_q[lo:hi], seeds[lo:hi], args.k, eps, args.expansion,
                                      lut[lo:hi], sc[lo:hi], to[lo:hi], threads=threads, L=L)
         return O.search_batch(metric, h_rows, h_off, h_edges, h_q[lo:hi], seeds[lo:hi], args.k, np.float32(eps),
-                              edge_size=0, threads=threads, L=L)
+                              edge_size=es_resolved, threads=threads, L=L)
 
     # size the sample to the time budget from a short probe
     nq = h_q.shape[0]

@@ -14,7 +14,11 @@
  * Threading: any number of threads may search one handle concurrently, as with
  * the reference (Capi.cpp:377-406).  Concurrent single-query calls with equal
  * parameters are coalesced into one device launch (ngt_amd/csrc/coalesce.h;
- * NGT_AMD_COALESCE=0 turns it off).
+ * NGT_AMD_COALESCE=0 turns it off).  Appends, inserts and ngt_create_index on a
+ * handle are serialized against its searches (a reader/writer lock: a write
+ * waits for the searches in flight, later searches wait for the write and see
+ * its objects); the reference itself leaves writes concurrent with searches
+ * undefined.
  *
  * Extensions (not in the reference): ngt_batch_search_index*,
  * ngt_get_last_search_counters, ngt_get_coalesce_stats.

@@ -147,6 +147,14 @@ int ngt_amd_search(ngt_amd_index *index, const ngt_amd_search_params *params,
                    uint64_t *counters);
 /* Device pointers; queries are already padded rows of the object type
  * (query_bytes apart) and already normalized where the metric requires it. */
+/* The tree seeds of nq prepared device queries: GraphAndTreeIndex::
+ * getSeedsFromTree (lib/NGT/Index.h:1524-1567) -- DVP-tree leaf descent
+ * (Tree.cpp:400-563) and the srand(leafID) thinning to min(seedSize, k) --
+ * into d_seeds [nq][seed_stride >= 128] and d_count [nq]: the seed lists a
+ * NGT_AMD_SEED_TREE search starts from, for callers that keep them. */
+int ngt_amd_tree_seeds_device(ngt_amd_index *index, const void *d_queries, uint64_t query_bytes, uint32_t nq,
+                              uint32_t k, uint32_t *d_seeds, uint32_t seed_stride, uint32_t *d_count,
+                              void *stream);
 int ngt_amd_search_device(ngt_amd_index *index, const ngt_amd_search_params *params,
                           const void *d_queries, uint64_t query_bytes, uint32_t nq,
                           const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,
@@ -266,15 +274,24 @@ int ngt_amd_merge_packed_device(int device, const uint64_t *d_packed, uint32_t n
  * k best over the union by (distance, global id) (Common.h:1937-1992).
  * ngt_amd_shard_unique_id fills an RCCL unique id (>= 128 bytes) on one rank;
  * the caller distributes it and every rank creates its communicator with it.
- * id_offsets: host array of every rank's offset.  One call at a time per
- * communicator.  Replaces nothing in the reference (NGT has no multi-GPU
- * form); the per-shard searches replace NGT::Index::search /
- * NGTQG::Index::search. */
+ * id_offsets: host array of every rank's offset -- the call then copies it
+ * and synchronizes before returning -- or NULL after
+ * ngt_amd_shard_comm_set_offsets stored them on the device: the call then only
+ * enqueues (search, pack, all-gather, merge on `stream`), so the exchange of
+ * one batch overlaps the search of the next; ngt_amd_shard_comm_synchronize
+ * waits and reports.  Each shard's device error flag (unchecked-set spill
+ * overflow) travels with its all-gathered message, so every rank fails the
+ * batch (at its return or at its synchronize) when any shard's list was
+ * truncated.  One call at a time per communicator, and asynchronous calls on
+ * one stream.  Replaces nothing in the reference (NGT has no multi-GPU form);
+ * the per-shard searches replace NGT::Index::search / NGTQG::Index::search. */
 typedef struct ngt_amd_shard_comm ngt_amd_shard_comm;
 int ngt_amd_shard_unique_id(uint8_t *id, uint64_t id_bytes);
 int ngt_amd_shard_comm_create(ngt_amd_shard_comm **comm, int device, int rank, int world,
                               const uint8_t *id, uint64_t id_bytes);
 int ngt_amd_shard_comm_destroy(ngt_amd_shard_comm *comm);
+int ngt_amd_shard_comm_set_offsets(ngt_amd_shard_comm *comm, const uint32_t *id_offsets);
+int ngt_amd_shard_comm_synchronize(ngt_amd_shard_comm *comm, void *stream);
 int ngt_amd_sharded_search_device(ngt_amd_shard_comm *comm, ngt_amd_index *index,
                                   const ngt_amd_search_params *params, const void *d_queries,
                                   uint64_t query_bytes, uint32_t nq, const uint32_t *d_seeds,

@@ -64,6 +64,7 @@ def declare(L):
         "ngt_amd_index_set_search_property": (c_int, [vp, c_int32, c_int32, c_int32, c_int32, c_int32]),
         "ngt_amd_resolve_edge_size": (c_uint64, [vp, c_int64, c_float]),
         "ngt_amd_search": (c_int, [vp, POINTER(SearchParams), vp, c_uint32, vp, vp, vp, vp, vp, vp]),
+        "ngt_amd_tree_seeds_device": (c_int, [vp, vp, c_uint64, c_uint32, c_uint32, vp, c_uint32, vp, vp]),
         "ngt_amd_search_device": (c_int, [vp, POINTER(SearchParams), vp, c_uint64, c_uint32, vp, vp, vp, vp,
                                           vp, vp, vp]),
         "ngt_amd_linear_search": (c_int, [vp, vp, c_uint32, c_uint32, c_double, vp, vp, vp]),
@@ -91,6 +92,8 @@ def declare(L):
         "ngt_amd_shard_unique_id": (c_int, [vp, c_uint64]),
         "ngt_amd_shard_comm_create": (c_int, [vp, c_int, c_int, c_int, vp, c_uint64]),
         "ngt_amd_shard_comm_destroy": (c_int, [vp]),
+        "ngt_amd_shard_comm_set_offsets": (c_int, [vp, vp]),
+        "ngt_amd_shard_comm_synchronize": (c_int, [vp, vp]),
         "ngt_amd_sharded_search_device": (c_int, [vp, vp, vp, vp, c_uint64, c_uint32, vp, vp, vp, vp, vp, vp, vp]),
         "ngt_amd_sharded_qg_search_device": (c_int, [vp, vp, vp, vp, c_uint64, c_uint32, vp, vp, vp, vp, vp, vp,
                                                      vp]),

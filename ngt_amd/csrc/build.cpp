@@ -118,6 +118,9 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
   HIP_OK(ix->adj.alloc((size_t)ix->nrows * b->adj_stride));
   HIP_OK(hipMemset(ix->adj.p, 0, (size_t)ix->nrows * b->adj_stride * sizeof(uint32_t)));
   ix->adj_stride = b->adj_stride;
+  // the construction's searches read at most adj_stride edges of a list: the
+  // padded copy is always the one to use (run_search never rebuilds it here)
+  ix->max_degree = b->adj_stride;
   ix->has_graph = true;
   ix->edge_size_for_search = prm->edge_size_for_search;
   ix->seed_size = prm->seed_size;

@@ -14,6 +14,7 @@
 #include <iostream>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -32,7 +33,11 @@ struct CapiIndex {
   HostIndex host;
   ngt_amd_index* dev = nullptr;
   bool device_stale = true;
-  std::mutex mu;                           // device (re)build and host mutations
+  // Searches hold `rw` shared from the device check to the end of their
+  // device call; appends/inserts, construction and the device rebuild hold it
+  // exclusively, so a rebuild never frees rows a running batch still reads.
+  std::shared_mutex rw;
+  std::mutex mu;                           // the coalescer's lazy creation
   std::unique_ptr<ngt_amd::Coalescer> co;  // concurrent single-query callers
   ~CapiIndex() {
     if (dev) ngt_amd_index_destroy(dev);
@@ -69,9 +74,9 @@ bool param_error(NGTError error, const char* func, const std::string& what) {
 
 std::string amd_err() { return std::string(ngt_amd_last_error()); }
 
-// Build / refresh the device index from the host mirror.
-std::string sync_device(CapiIndex* ix) {
-  std::lock_guard<std::mutex> lk(ix->mu);
+// Build / refresh the device index from the host mirror (caller holds `rw`
+// exclusively).
+std::string rebuild_device(CapiIndex* ix) {
   if (!ix->device_stale && ix->dev) return "";
   HostIndex& h = ix->host;
   if (h.nrows < 2) return "the index is empty";
@@ -101,6 +106,19 @@ std::string sync_device(CapiIndex* ix) {
   return "";
 }
 
+// A current device copy, with `rd` holding `rw` shared on success: the copy
+// cannot be rebuilt under the caller until `rd` is released.
+std::string sync_device(CapiIndex* ix, std::shared_lock<std::shared_mutex>& rd) {
+  for (;;) {
+    rd = std::shared_lock<std::shared_mutex>(ix->rw);
+    if (!ix->device_stale && ix->dev) return "";
+    rd.unlock();
+    std::unique_lock<std::shared_mutex> wl(ix->rw);
+    std::string e = rebuild_device(ix);
+    if (!e.empty()) return e;
+  }
+}
+
 bool use_tree(CapiIndex* ix) { return ix->host.prop.index_type == 0 && ix->host.tree.present; }
 
 // One batched search: the single-query API is a batch of one.
@@ -108,7 +126,8 @@ std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t 
                        float radius, int64_t edge_size, int seed_mode, std::vector<uint32_t>& ids,
                        std::vector<float>& dists, std::vector<uint32_t>& n,
                        std::vector<uint64_t>* per_query = nullptr) {
-  std::string e = sync_device(ix);
+  std::shared_lock<std::shared_mutex> rd;
+  std::string e = sync_device(ix, rd);
   if (!e.empty()) return e;
   if (size == 0) {
     // GraphIndex::search with sc.size == 0 returns nothing (Index.h:1141-1144)
@@ -152,7 +171,8 @@ std::string run_search(CapiIndex* ix, const float* queries, uint32_t nq, size_t 
 std::string run_linear(CapiIndex* ix, const float* queries, uint32_t nq, size_t size,
                        std::vector<uint32_t>& ids, std::vector<float>& dists, std::vector<uint32_t>& n,
                        double radius = (double)FLT_MAX) {
-  std::string e = sync_device(ix);
+  std::shared_lock<std::shared_mutex> rd;
+  std::string e = sync_device(ix, rd);
   if (!e.empty()) return e;
   if (size == 0) {
     n.assign(nq, 0);
@@ -219,7 +239,7 @@ std::string normalize_row(T* data, uint32_t dim) {
 // (ObjectSpaceRepository.h:560-566).
 template <typename T>
 std::string append_object(CapiIndex* ix, const T* obj, uint32_t dim, uint32_t& id) {
-  std::lock_guard<std::mutex> lk(ix->mu);
+  std::unique_lock<std::shared_mutex> wl(ix->rw);
   HostIndex& h = ix->host;
   const bool sparse = h.prop.distance_type == 8;
   // a sparse object (0-terminated id list, Index::makeSparseObject) may be
@@ -256,6 +276,7 @@ std::string append_object(CapiIndex* ix, const T* obj, uint32_t dim, uint32_t& i
 // build: ANNG with the tree, on the device; the host mirror receives the
 // graph (CSR + distances) and the DVP tree for ngt_save_index and searches.
 std::string build_anng(CapiIndex* ix) {
+  std::unique_lock<std::shared_mutex> wl(ix->rw);
   HostIndex& h = ix->host;
   if (h.prop.edge_size_for_creation == 0) return "";  // createIndex returns at once (Index.cpp:1162-1164)
   if (h.prop.graph_type != 1) return "index construction supports graphType ANNG only";
@@ -265,7 +286,7 @@ std::string build_anng(CapiIndex* ix) {
     has_graph = h.edge_off[v + 1] != h.edge_off[v];
   if (has_graph && !h.tree.present) return "the index has a graph but no DVP tree";
   if (h.nrows < 2) return "";
-  std::string e = sync_device(ix);
+  std::string e = rebuild_device(ix);
   if (!e.empty()) return e;
   ngt_amd_build_params p{};
   p.edge_size_for_creation = h.prop.edge_size_for_creation;
@@ -403,7 +424,9 @@ bool ngt_save_index(const NGTIndex index, const char* database, NGTError error) 
     return false;
   }
   mkdir(database, 0755);
-  std::string e = ngt_amd::save_index(database, static_cast<CapiIndex*>(index)->host);
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  std::shared_lock<std::shared_mutex> rd(ix->rw);  // no append/insert/build while the mirror is written out
+  std::string e = ngt_amd::save_index(database, ix->host);
   if (!e.empty()) {
     set_error(error, __FUNCTION__, e);
     return false;

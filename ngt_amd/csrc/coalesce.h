@@ -95,19 +95,33 @@ class Coalescer {
           }
         }
         lk.unlock();
-        std::vector<float> qs(batch.size() * (size_t)dim_);
-        for (size_t i = 0; i < batch.size(); i++) memcpy(qs.data() + i * dim_, batch[i]->query, dim_ * sizeof(float));
-        try {
-          runner(k, qs.data(), (uint32_t)batch.size(), batch);
-        } catch (std::exception& e) {
-          for (auto* b : batch) b->err = e.what();
+        {
+          // whatever the runner does (returns, throws anything), the batch is
+          // marked done, the leader slot freed and the waiters woken
+          struct Finish {
+            Coalescer* self;
+            std::unique_lock<std::mutex>& lk;
+            std::vector<CoalesceReq*>& batch;
+            ~Finish() {
+              lk.lock();
+              self->batches_++;
+              self->served_ += batch.size();
+              for (auto* b : batch) b->done = true;
+              self->leaders_--;
+              self->cv_.notify_all();
+            }
+          } fin{this, lk, batch};
+          try {
+            std::vector<float> qs(batch.size() * (size_t)dim_);
+            for (size_t i = 0; i < batch.size(); i++)
+              memcpy(qs.data() + i * dim_, batch[i]->query, dim_ * sizeof(float));
+            runner(k, qs.data(), (uint32_t)batch.size(), batch);
+          } catch (std::exception& e) {
+            for (auto* b : batch) b->err = e.what();
+          } catch (...) {
+            for (auto* b : batch) b->err = "search failed with a non-standard exception";
+          }
         }
-        lk.lock();
-        batches_++;
-        served_ += batch.size();
-        for (auto* b : batch) b->done = true;
-        leaders_--;
-        cv_.notify_all();
         continue;
       }
       cv_.wait(lk);

@@ -72,6 +72,8 @@ extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distanc
   ix->dp = ((dimension - 1) / 16 + 1) * 16;
   ix->esize = object_type == 2 ? 4 : 1;
   ix->row_bytes = (uint64_t)ix->dp * ix->esize;
+  // test hook: a tiny unchecked-set spill makes the overflow flag reachable
+  if (const char* v = getenv("NGT_AMD_SPILL_CAP")) ix->spill_cap = (uint32_t)std::max(1, atoi(v));
   ix->cu_count = prop.multiProcessorCount;
   ix->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
   ix->lds_per_block = prop.sharedMemPerBlock ? prop.sharedMemPerBlock : 64 * 1024;
@@ -134,22 +136,47 @@ static void note_graph_empty(ngt_amd_index* ix, const uint64_t* offsets, uint64_
   for (uint64_t i = 0; i < nrows; i++) ix->h_graph_empty[i] = offsets[i + 1] == offsets[i];
 }
 
-// Padded adjacency [nrows][stride] (0-terminated rows) built on the device from
-// the CSR: one load per edge chunk instead of an offset load followed by a
-// dependent edge load.  Kept only while the widest node is <= 256 edges.
-static int build_padded_adjacency(ngt_amd_index* ix, const uint64_t* h_offsets) {
-  uint64_t maxdeg = 0;
-  for (uint64_t i = 0; i < ix->nrows; i++) maxdeg = std::max<uint64_t>(maxdeg, h_offsets[i + 1] - h_offsets[i]);
-  ix->max_degree = maxdeg;
+// Padded adjacency [nrows][W] built on the device from the CSR: the first W
+// edges of every list (W a multiple of 16, at most 256), 0-terminated when
+// shorter -- one load per expansion instead of an offset load followed by a
+// dependent edge load.  A search reads min(degree, edgeSize) edges of a list
+// (Graph.cpp:436-439, getEdgeSize Graph.h:675-692), so the copy serves every
+// search with min(max degree, edgeSize) <= W: an NGT index's hubs (an ANNG's
+// reverse edges give some nodes hundreds) do not matter at its
+// EdgeSizeForSearch of 40.  W grows on demand; searches needing more than 256
+// edges of a list take the CSR path.
+static int build_padded_adjacency(ngt_amd_index* ix, uint64_t need) {
+  if (need == 0 || need > 256) return 0;
+  if (ix->adj.p && ix->adj_stride >= need) return 0;
+  const uint64_t stride = (need + 15) & ~15ull;
   ix->adj.release();
   ix->adj_stride = 0;
-  if (maxdeg == 0 || maxdeg > 256) return 0;
-  uint64_t stride = (maxdeg + 15) & ~15ull;
   HIP_OK(ix->adj.alloc(ix->nrows * stride));
   HIP_OK(launch_pad_adjacency(ix->edge_off.p, ix->edges.p, ix->nrows, stride, ix->adj.p, ix->stream));
   HIP_OK(hipStreamSynchronize(ix->stream));
   ix->adj_stride = stride;
   return 0;
+}
+
+static uint64_t max_degree_of(const uint64_t* h_offsets, uint64_t nrows) {
+  uint64_t maxdeg = 0;
+  for (uint64_t i = 0; i < nrows; i++) maxdeg = std::max<uint64_t>(maxdeg, h_offsets[i + 1] - h_offsets[i]);
+  return maxdeg;
+}
+
+// edges a search with resolved edge size `es` reads of the widest list
+static uint64_t adjacency_need(const ngt_amd_index* ix, uint64_t es) {
+  return std::min<uint64_t>(ix->max_degree, es);
+}
+
+static int reset_adjacency(ngt_amd_index* ix, const uint64_t* h_offsets) {
+  ix->max_degree = max_degree_of(h_offsets, ix->nrows);
+  ix->adj.release();
+  ix->adj_stride = 0;
+  // sized for the index's own EdgeSizeForSearch now; grown if a search asks for more
+  const int64_t es = ix->edge_size_for_search;
+  const uint64_t want = es > 0 ? (uint64_t)es : (uint64_t)INT_MAX;
+  return build_padded_adjacency(ix, adjacency_need(ix, want));
 }
 
 extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offsets,
@@ -166,7 +193,7 @@ extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offset
   ix->nedges = nedges;
   ix->has_graph = true;
   note_graph_empty(ix, offsets, ix->nrows);
-  return build_padded_adjacency(ix, offsets);
+  return reset_adjacency(ix, offsets);
 }
 
 extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t* d_offsets,
@@ -184,7 +211,7 @@ extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t*
   std::vector<uint64_t> h(ix->nrows + 1);
   HIP_OK(hipMemcpy(h.data(), d_offsets, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   note_graph_empty(ix, h.data(), ix->nrows);
-  return build_padded_adjacency(ix, h.data());
+  return reset_adjacency(ix, h.data());
 }
 
 extern "C" int ngt_amd_index_set_tree(ngt_amd_index* ix, const void* in_pivot, uint32_t n_internal,
@@ -402,8 +429,15 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   a.dp = (int)ix->dp;
   a.edge_off = ix->edge_off.p;
   a.edges = ix->edges.p;
-  a.adj = ix->adj.p;
-  a.adj_stride = ix->adj_stride;
+  {
+    // the padded copy, when it holds every edge this search reads
+    const uint64_t need = adjacency_need(ix, es);
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (build_padded_adjacency(ix, need)) return -1;
+    const bool fits = ix->adj.p && need <= ix->adj_stride;
+    a.adj = fits ? ix->adj.p : nullptr;
+    a.adj_stride = fits ? ix->adj_stride : 0;
+  }
   if (const char* v = getenv("NGT_AMD_ADJ"))
     if (atoi(v) == 0) a.adj = nullptr;
   a.queries = static_cast<const uint8_t*>(d_queries);
@@ -609,6 +643,25 @@ extern "C" int ngt_amd_search_device(ngt_amd_index* ix, const ngt_amd_search_par
   }
   return run_search(ix, c, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, d_ids, d_dists,
                     d_n, d_counters, s);
+}
+
+extern "C" int ngt_amd_tree_seeds_device(ngt_amd_index* ix, const void* d_queries, uint64_t query_bytes, uint32_t nq,
+                                         uint32_t k, uint32_t* d_seeds, uint32_t seed_stride, uint32_t* d_count,
+                                         void* stream) {
+  if (!ix || (!d_queries && nq) || !d_seeds || !d_count || k == 0 || seed_stride < kTreeSeedStride)
+    return fail("ngt_amd_tree_seeds_device: bad arguments (seed_stride must be >= %u)", kTreeSeedStride);
+  if (nq && query_bytes < ix->row_bytes) return fail("ngt_amd_tree_seeds_device: query stride too small");
+  if (nq == 0) return 0;
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = (hipStream_t)stream;
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
+  if (run_tree_seeds(ix, c, d_queries, query_bytes, nq, k, 0, s)) return -1;
+  HIP_OK(hipMemcpy2DAsync(d_seeds, (size_t)seed_stride * sizeof(uint32_t), c->seeds.p,
+                          (size_t)kTreeSeedStride * sizeof(uint32_t), (size_t)kTreeSeedStride * sizeof(uint32_t), nq,
+                          hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemcpyAsync(d_count, c->seed_count.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  return 0;
 }
 
 extern "C" int ngt_amd_last_search_filtered(const ngt_amd_index* ix) {

@@ -115,6 +115,10 @@ struct MergeArgs {
   uint32_t* out_ids;             // [nq][k] global ids
   float* out_dists;
   uint32_t* out_n;               // [nq]
+  // packed merge only: words between parts (0: nq * k) and, when non-null,
+  // the flag ORed with every part's trailer word (packed[part * stride + nq * k])
+  uint64_t part_stride;
+  int* err_out;
 };
 
 // ---- ANNG construction (build_kernels.hip) ----------------------------------

@@ -765,10 +765,15 @@ __global__ void __launch_bounds__(64) ngt_merge_packed_kernel(MergeArgs a, const
   uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
   const int lane = lane_id();
   const uint32_t total = a.nparts * a.k;
+  const uint64_t stride = a.part_stride ? a.part_stride : (uint64_t)a.nq * a.k;
+  if (a.err_out && blockIdx.x == 0 && (uint32_t)lane < a.nparts) {
+    const int f = (int)(uint32_t)packed[(uint64_t)lane * stride + (uint64_t)a.nq * a.k];
+    if (f) atomicOr(a.err_out, f);
+  }
   for (uint32_t qi = blockIdx.x; qi < a.nq; qi += gridDim.x) {
     for (uint32_t i = lane; i < total; i += 64) {
       const uint32_t s = i / a.k, j = i - s * a.k;
-      const uint64_t w = packed[((uint64_t)s * a.nq + qi) * a.k + j];
+      const uint64_t w = packed[(uint64_t)s * stride + (uint64_t)qi * a.k + j];
       const uint32_t id = (uint32_t)w;
       keys[i] = id ? make_key(__uint_as_float((uint32_t)(w >> 32)), id + a.id_offsets[s]) : ~0ull;
     }

@@ -26,6 +26,8 @@ struct ngt_amd_shard_comm {
   DevBuf<uint32_t> ids, n, off;
   DevBuf<float> dists;
   DevBuf<uint64_t> packed, gathered;
+  DevBuf<int> err;         // OR of every shard's device error flag since the last synchronize
+  bool have_offsets = false;
 };
 
 #define NCCL_OK(expr)                                                                       \
@@ -53,6 +55,10 @@ extern "C" int ngt_amd_shard_comm_create(ngt_amd_shard_comm** out, int device, i
   c->device = device;
   c->rank = rank;
   c->world = world;
+  if (c->err.alloc(1) != hipSuccess || hipMemset(c->err.p, 0, sizeof(int)) != hipSuccess) {
+    delete c;
+    return fail("ngt_amd_shard_comm_create: allocation failed");
+  }
   ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
   if (r != ncclSuccess) {
     delete c;
@@ -70,18 +76,38 @@ extern "C" int ngt_amd_shard_comm_destroy(ngt_amd_shard_comm* c) {
   return 0;
 }
 
-// pack -> all-gather -> merge of this rank's [nq][k] lists (already searched)
-static int exchange_and_merge(ngt_amd_shard_comm* c, uint32_t nq, uint32_t k, const uint32_t* id_offsets,
-                              uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_out_n, hipStream_t s) {
+// pack -> all-gather -> merge of this rank's [nq][k] lists (already searched
+// on stream s with launch context `ctx`).  Every rank's message carries one
+// trailer word after its nq*k result words: that shard's device error flag
+// (unchecked-set spill overflow), taken from its launch context and cleared
+// there, so a truncated shard list is reported on EVERY rank -- the merge ORs
+// the trailers into c->err.  With id_offsets == NULL (offsets stored by
+// ngt_amd_shard_comm_set_offsets) nothing here waits for the device: the
+// all-gather of one batch overlaps the next batch's search, and
+// ngt_amd_shard_comm_synchronize reports the flags.  With a host id_offsets
+// array (the original form) the call copies it, synchronizes and reports.
+static int exchange_and_merge(ngt_amd_shard_comm* c, ngt_amd_index* ix, uint32_t nq, uint32_t k,
+                              const uint32_t* id_offsets, uint32_t* d_out_ids, float* d_out_dists,
+                              uint32_t* d_out_n, hipStream_t s) {
   if ((uint64_t)c->world * k * sizeof(uint64_t) > 64 * 1024)
     return fail("sharded search: %d shards x k=%u exceed one workgroup's LDS in the merge", c->world, k);
-  const uint64_t words = (uint64_t)nq * k;
-  HIP_OK(c->packed.alloc(words));
-  HIP_OK(c->gathered.alloc(words * c->world));
-  HIP_OK(c->off.alloc(c->world));
+  if (!id_offsets && !c->have_offsets)
+    return fail("sharded search: no id offsets (pass them, or set them once with ngt_amd_shard_comm_set_offsets)");
+  SearchCtx* ctx = ctx_for(ix, s);
+  if (!ctx) return -1;
+  const uint64_t words = (uint64_t)nq * k, stride = words + 1;
+  HIP_OK(c->packed.alloc(stride));
+  HIP_OK(c->gathered.alloc(stride * c->world));
   HIP_OK(launch_pack_results(c->ids.p, c->dists.p, c->n.p, nq, k, c->packed.p, s));
-  NCCL_OK(ncclAllGather(c->packed.p, c->gathered.p, words, ncclUint64, c->comm, s));
-  HIP_OK(hipMemcpyAsync(c->off.p, id_offsets, c->world * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemsetAsync(c->packed.p + words, 0, sizeof(uint64_t), s));
+  HIP_OK(hipMemcpyAsync(c->packed.p + words, ctx->err.p, sizeof(int), hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemsetAsync(ctx->err.p, 0, sizeof(int), s));
+  NCCL_OK(ncclAllGather(c->packed.p, c->gathered.p, stride, ncclUint64, c->comm, s));
+  if (id_offsets) {
+    HIP_OK(c->off.alloc(c->world));
+    HIP_OK(hipMemcpyAsync(c->off.p, id_offsets, c->world * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    c->have_offsets = false;  // the caller's array, not a stored set
+  }
   MergeArgs a{};
   a.id_offsets = c->off.p;
   a.nparts = (uint32_t)c->world;
@@ -90,9 +116,35 @@ static int exchange_and_merge(ngt_amd_shard_comm* c, uint32_t nq, uint32_t k, co
   a.out_ids = d_out_ids;
   a.out_dists = d_out_dists;
   a.out_n = d_out_n;
+  a.part_stride = stride;
+  a.err_out = c->err.p;
   HIP_OK(launch_merge_packed(a, c->gathered.p, s));
-  // the offsets were copied from the caller's host array: done before return
+  if (!id_offsets) return 0;
+  // the offsets came from the caller's host array: done before return
+  return ngt_amd_shard_comm_synchronize(c, s);
+}
+
+extern "C" int ngt_amd_shard_comm_set_offsets(ngt_amd_shard_comm* c, const uint32_t* id_offsets) {
+  if (!c || !id_offsets) return fail("ngt_amd_shard_comm_set_offsets: bad arguments");
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(c->off.upload(id_offsets, (size_t)c->world));
+  c->have_offsets = true;
+  return 0;
+}
+
+extern "C" int ngt_amd_shard_comm_synchronize(ngt_amd_shard_comm* c, void* stream) {
+  if (!c) return fail("ngt_amd_shard_comm_synchronize: null communicator");
+  HIP_OK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  int flag = 0;
+  HIP_OK(hipMemcpyAsync(&flag, c->err.p, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  if (flag) {
+    HIP_OK(hipMemsetAsync(c->err.p, 0, sizeof(int), s));
+    HIP_OK(hipStreamSynchronize(s));
+    return fail("sharded search: a shard's search flagged device error %d (unchecked-set spill capacity "
+                "exceeded): its result list was truncated", flag);
+  }
   return 0;
 }
 
@@ -102,7 +154,7 @@ extern "C" int ngt_amd_sharded_search_device(ngt_amd_shard_comm* c, ngt_amd_inde
                                              const uint64_t* d_seed_off, const uint32_t* id_offsets,
                                              uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_out_n,
                                              void* stream) {
-  if (!c || !ix || !prm || !id_offsets || !d_out_ids || !d_out_dists || !d_out_n || prm->k == 0)
+  if (!c || !ix || !prm || !d_out_ids || !d_out_dists || !d_out_n || prm->k == 0)
     return fail("ngt_amd_sharded_search_device: bad arguments");
   HIP_OK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
@@ -112,7 +164,7 @@ extern "C" int ngt_amd_sharded_search_device(ngt_amd_shard_comm* c, ngt_amd_inde
   if (ngt_amd_search_device(ix, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, c->ids.p, c->dists.p, c->n.p,
                             nullptr, stream))
     return -1;
-  return exchange_and_merge(c, nq, prm->k, id_offsets, d_out_ids, d_out_dists, d_out_n, s);
+  return exchange_and_merge(c, ix, nq, prm->k, id_offsets, d_out_ids, d_out_dists, d_out_n, s);
 }
 
 extern "C" int ngt_amd_sharded_qg_search_device(ngt_amd_shard_comm* c, ngt_amd_index* ix,
@@ -121,7 +173,7 @@ extern "C" int ngt_amd_sharded_qg_search_device(ngt_amd_shard_comm* c, ngt_amd_i
                                                 const uint64_t* d_seed_off, const uint32_t* id_offsets,
                                                 uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_out_n,
                                                 void* stream) {
-  if (!c || !ix || !prm || !id_offsets || !d_out_ids || !d_out_dists || !d_out_n || prm->k == 0)
+  if (!c || !ix || !prm || !d_out_ids || !d_out_dists || !d_out_n || prm->k == 0)
     return fail("ngt_amd_sharded_qg_search_device: bad arguments");
   HIP_OK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
@@ -131,5 +183,5 @@ extern "C" int ngt_amd_sharded_qg_search_device(ngt_amd_shard_comm* c, ngt_amd_i
   if (ngt_amd_qg_search_device(ix, prm, d_queries, query_bytes, nq, d_seeds, d_seed_off, c->ids.p, c->dists.p,
                                c->n.p, nullptr, stream))
     return -1;
-  return exchange_and_merge(c, nq, prm->k, id_offsets, d_out_ids, d_out_dists, d_out_n, s);
+  return exchange_and_merge(c, ix, nq, prm->k, id_offsets, d_out_ids, d_out_dists, d_out_n, s);
 }

@@ -19,6 +19,8 @@ The exchange is backend-agnostic (torch.distributed collectives on tensors of
 the merge's device); the CPU tests run it over ``gloo`` with numpy stand-ins
 for the two device kernels (``pack=`` / ``merge=``).
 """
+import contextlib
+
 import numpy as np
 
 from . import NativeError, lib
@@ -108,22 +110,35 @@ class ShardedIndex(object):
         self.pack = pack
         self.merge = merge
 
+    @contextlib.contextmanager
+    def _on(self, stream):
+        """Context in which torch's current stream is `stream` (a raw HIP
+        stream handle), so every allocation, fill and collective below is
+        ordered with the library's launches on it; yields that torch stream
+        (None on CPU tensors or without a stream)."""
+        if stream is None or getattr(self.device, "type", "cpu") != "cuda":
+            yield None
+            return
+        ext = self.torch.cuda.ExternalStream(stream, device=self.device)
+        with self.torch.cuda.stream(ext):
+            yield ext
+
     def merge_local(self, ids, dists, n, k, stream=None):
         """Pack, exchange (one all-gather) and merge already computed local
-        results (tensors [nq, k], [nq, k], [nq])."""
+        results (tensors [nq, k], [nq, k], [nq], written on `stream`).  The
+        packed words, the gathered buffer and the merged outputs are allocated
+        with `stream` current, so their zero-fills, the pack, the collective
+        and the merge are all ordered on it; the inputs are recorded on it so
+        the caching allocator cannot hand their memory out while it still
+        reads them."""
         t = self.torch
-        packed = self.pack(t, ids, dists, n, k, stream)
-        ext = None
-        if stream is not None and ids.is_cuda:
-            # the collective is ordered after torch's current stream: make that
-            # stream wait for the search + pack on `stream`, and the merge wait
-            # for the collective
-            ext = t.cuda.ExternalStream(stream, device=self.device)
-            t.cuda.current_stream(self.device).wait_stream(ext)
-        g = exchange_packed(t, self.dist, packed)
-        if ext is not None:
-            ext.wait_stream(t.cuda.current_stream(self.device))
-        return self.merge(t, g, self.offsets, k, stream)
+        with self._on(stream) as st:
+            if st is not None:
+                for x in (ids, dists, n):
+                    x.record_stream(st)
+            packed = self.pack(t, ids, dists, n, k, stream)
+            g = exchange_packed(t, self.dist, packed)
+            return self.merge(t, g, self.offsets, k, stream)
 
     def _out(self, nq, k):
         t = self.torch
@@ -135,7 +150,8 @@ class ShardedIndex(object):
         """Local graph search of nq device queries on this shard, then the
         exchange and merge; returns global (ids, dists, n) tensors."""
         from .device import SEED_GIVEN, SEED_TREE
-        ids, ds, n = self._out(nq, k)
+        with self._on(stream):  # the outputs' zero-fill is ordered before the search on `stream`
+            ids, ds, n = self._out(nq, k)
         mode = seed_mode if seed_mode is not None else (SEED_GIVEN if seeds is not None else SEED_TREE)
         self.index.search_device(d_queries, query_bytes, nq, ids.data_ptr(), ds.data_ptr(), n.data_ptr(), None,
                                  k=k, epsilon=epsilon, edge_size=edge_size, seed_mode=mode, d_seeds=seeds,
@@ -148,7 +164,8 @@ class ShardedIndex(object):
         queries on this shard's quantized graph (exact rerank of k * expansion
         included), then the same exchange and merge of the reranked top-k."""
         from .device import SEED_GIVEN, SEED_TREE
-        ids, ds, n = self._out(nq, k)
+        with self._on(stream):
+            ids, ds, n = self._out(nq, k)
         mode = seed_mode if seed_mode is not None else (SEED_GIVEN if seeds is not None else SEED_TREE)
         self.index.qg_search_device(d_queries, query_bytes, nq, ids.data_ptr(), ds.data_ptr(), n.data_ptr(), None,
                                     k=k, epsilon=epsilon, result_expansion=result_expansion, seed_mode=mode,
@@ -182,20 +199,35 @@ class RcclShardComm(object):
         if self.L.ngt_amd_shard_comm_create(ctypes.byref(self.h), device, rank, world, buf, len(uid)) != 0:
             raise NativeError(self.L.ngt_amd_last_error().decode())
 
+    def set_offsets(self, offsets):
+        """Store every rank's id offset on the device once; later searches
+        pass offsets=None and only enqueue (ngt_amd_shard_comm_set_offsets)."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        if self.L.ngt_amd_shard_comm_set_offsets(self.h, off.ctypes.data) != 0:
+            raise NativeError(self.L.ngt_amd_last_error().decode())
+
+    def synchronize(self, stream=None):
+        """Wait for the enqueued sharded searches; raises if any shard's
+        search overflowed (ngt_amd_shard_comm_synchronize)."""
+        if self.L.ngt_amd_shard_comm_synchronize(self.h, stream) != 0:
+            raise NativeError(self.L.ngt_amd_last_error().decode())
+
     def search_device(self, index, d_queries, query_bytes, nq, offsets, d_ids, d_dists, d_n, k=10, epsilon=0.1,
                       radius=-1.0, edge_size=-1, seed_mode=0, d_seeds=None, d_seed_off=None, stream=None,
                       visited_hash_log2=0, qg=False, result_expansion=3.0):
+        """offsets: every rank's id offset (copied, and the call synchronizes),
+        or None after set_offsets (the call only enqueues)."""
         import ctypes
         from ._sigs import QgSearchParams, SearchParams
-        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        off = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint32)
         if qg:
             prm = QgSearchParams(k, epsilon, result_expansion, radius, seed_mode, visited_hash_log2)
             fn = self.L.ngt_amd_sharded_qg_search_device
         else:
             prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, visited_hash_log2, 0)
             fn = self.L.ngt_amd_sharded_search_device
-        if fn(self.h, index.h, ctypes.byref(prm), d_queries, query_bytes, nq, d_seeds, d_seed_off, off.ctypes.data,
-              d_ids, d_dists, d_n, stream) != 0:
+        if fn(self.h, index.h, ctypes.byref(prm), d_queries, query_bytes, nq, d_seeds, d_seed_off,
+              None if off is None else off.ctypes.data, d_ids, d_dists, d_n, stream) != 0:
             raise NativeError(self.L.ngt_amd_last_error().decode())
 
     def close(self):

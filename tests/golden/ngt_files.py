@@ -169,7 +169,9 @@ def parse_search_output(text):
     cur = None
     for line in text.splitlines():
         if line.startswith("# Query No."):
-            cur = {"ids": [], "dists": [], "ndist": 0, "nvisit": 0}
+            cur = {"ids": [], "dists": [], "ndist": 0, "nvisit": 0, "time_ms": 0.0}
+        elif line.startswith("# Query Time (msec)="):
+            cur["time_ms"] = float(line.split("=")[1])
         elif line.startswith("# Distance Computation="):
             cur["ndist"] = int(line.split("=")[1])
         elif line.startswith("# Visit Count="):

@@ -133,11 +133,23 @@ def test_sharded_index_one_rank_nccl():
         gi, gd, gn = sx.search_device(d_q.data_ptr(), dim * 4, nq, 10, 0.2, seeds=d_s.data_ptr(),
                                       seed_off=d_o.data_ptr(), stream=stream, edge_size=0, seed_mode=SEED_GIVEN)
         torch.cuda.synchronize()
+        ref_t = (gi.clone(), gd.clone(), gn.clone())
         gi, gd, gn = gi.cpu().numpy().view(np.uint32), gd.cpu().numpy(), gn.cpu().numpy()
         for i in range(nq):
             oid, od, _ = O.search("l2", rows, offs, edges, qs[i], seeds[i], 10, np.float32(0.2))
             assert list(gi[i, :gn[i]]) == list(oid + off), i
             assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od.view(np.uint32))
+        # the same search, pack, collective and merge on a side stream: outputs
+        # allocated and zero-filled there, inputs recorded on it (ngt_amd/shard.py)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        for _ in range(3):
+            si, sd, sn = sx.search_device(d_q.data_ptr(), dim * 4, nq, 10, 0.2, seeds=d_s.data_ptr(),
+                                          seed_off=d_o.data_ptr(), stream=side.cuda_stream, edge_size=0,
+                                          seed_mode=SEED_GIVEN)
+        side.synchronize()
+        assert torch.equal(si, ref_t[0]) and torch.equal(sd.view(torch.int32), ref_t[1].view(torch.int32))
+        assert torch.equal(sn, ref_t[2])
         ix.close()
 
         # C5's form: the NGTQG search on the shard, then the same exchange and
@@ -205,7 +217,46 @@ def test_rccl_sharded_search_c_abi():
             oid, odist, _ = O.search("l2", rows, offs, edges, qs[i], seeds[i], k, np.float32(0.2))
             assert list(gi[i, :gn[i]]) == list(oid + off), i
             assert np.array_equal(gd[i, :gn[i]].view(np.uint32), odist.view(np.uint32))
+
+        # asynchronous form: offsets stored once, two batches enqueued back to
+        # back on a side stream, one synchronize
+        comm.set_offsets([off])
+        side = torch.cuda.Stream(dev)
+        outs = [tuple(torch.full(sh, -1, dtype=dt, device=dev) for sh, dt in
+                      (((nq, k), torch.int32), ((nq, k), torch.float32), ((nq,), torch.int32))) for _ in range(2)]
+        side.wait_stream(torch.cuda.current_stream(dev))
+        for a, b, c in outs:
+            comm.search_device(ix, d_q.data_ptr(), dim * 4, nq, None, a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                               k=k, epsilon=0.2, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_s.data_ptr(),
+                               d_seed_off=d_o.data_ptr(), stream=side.cuda_stream)
+        comm.synchronize(side.cuda_stream)
+        for a, b, c in outs:
+            assert np.array_equal(a.cpu().numpy().view(np.uint32), gi)
+            assert np.array_equal(b.cpu().numpy().view(np.uint32), gd.view(np.uint32))
+            assert np.array_equal(c.cpu().numpy(), gn)
         ix.close()
+
+        # a shard whose unchecked-set spill overflows (capacity forced to one
+        # key): the flag travels with the all-gathered message and the
+        # synchronize reports it instead of a silently truncated list
+        from ngt_amd import NativeError
+        os.environ["NGT_AMD_SPILL_CAP"] = "1"
+        os.environ["NGT_AMD_CQ_CAP"] = "64"
+        try:
+            ix2 = DeviceIndex("l2", "float", dim)
+            ix2.set_objects(rows)
+            ix2.set_graph(offs, edges)
+            a, b, c = outs[0]
+            comm.search_device(ix2, d_q.data_ptr(), dim * 4, nq, None, a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                               k=k, epsilon=1.0, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_s.data_ptr(),
+                               d_seed_off=d_o.data_ptr(), stream=stream)
+            with pytest.raises(NativeError, match="truncated"):
+                comm.synchronize(stream)
+            comm.synchronize(stream)  # the flag is cleared once reported
+            ix2.close()
+        finally:
+            del os.environ["NGT_AMD_SPILL_CAP"]
+            del os.environ["NGT_AMD_CQ_CAP"]
 
         from test_gpu_qg import device_qg, state
         _, _, _, _, _, _, _, z, meta, dim, _ = state("c1_qg")
