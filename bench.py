@@ -195,7 +195,10 @@ def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.0005, la
             log("eps sweep: %.1f ms per launch at eps %.4f exceeds the %.0f ms cap; stopping" % (
                 last_ms(), hi, SWEEP_KERNEL_MS_CAP))
             return hi
-        lo, hi = hi, hi * 2
+        # a search's cost grows steeply with epsilon on high-dimensional data:
+        # double while launches are cheap, then creep up
+        grow = 2.0 if last_ms is None or last_ms() < SWEEP_KERNEL_MS_CAP / 100.0 else 1.25
+        lo, hi = hi, hi * grow
     while hi - lo > tol:
         mid = 0.5 * (lo + hi)
         if measure(mid) >= target:
@@ -239,6 +242,7 @@ def main():
     ap.add_argument("--expansion", type=float, default=3.0, help="NGTQG result_expansion")
     ap.add_argument("--qg-edges", type=int, default=128, help="NGTQG max edges per node")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--sweep-nq", type=int, default=2000, help="queries per epsilon-sweep launch")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
     ap.add_argument("--visited", type=int, default=-2,
@@ -399,18 +403,18 @@ def main():
         log("quantizer (k-means %d-%d iterations) + encoder + quantized graph in %.1f s (degree <= %d)" % (
             its.min(), its.max(), time.time() - t0, ix.qg_max_degree()))
 
-    def run(eps, si=0, visited=None):
+    def run(eps, si=0, visited=None, nq=NQ):
         oi, od, on, oc = bufs[si]
         visited = args.visited if visited is None else visited
         if qgm:
-            ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+            ix.qg_search_device(qdev.data_ptr(), dp * 4, nq, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
                                 oc.data_ptr(), k=K, epsilon=eps, result_expansion=args.expansion,
                                 seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
                                 stream=streams[si], visited_hash_log2=visited)
             if shard:
                 result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
             return
-        ix.search_device(qdev.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+        ix.search_device(qdev.data_ptr(), dp * 4, nq, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
                          oc.data_ptr(), k=K, epsilon=eps, edge_size=args.edge_size, seed_mode=SEED_GIVEN,
                          d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(), stream=streams[si],
                          visited_hash_log2=visited)
@@ -418,24 +422,34 @@ def main():
             result["ids"] = sx.merge_local(out_i, out_d, out_n, K, stream)[0]
 
     sweep = []
+    # the sweep runs on the first `sweep_nq` queries (shards: the whole batch,
+    # the merged recall needs every rank's results), the chosen epsilon is
+    # then checked on the whole batch and raised in small steps if needed
+    sweep_nq = NQ if shard else min(NQ, args.sweep_nq)
 
-    def measure(eps):
-        run(eps)
+    def measure(eps, nq=None):
+        nq = sweep_nq if nq is None else nq
+        run(eps, nq=nq)
         torch.cuda.synchronize()
-        r = recall_at(result["ids"].cpu().numpy(), gt, K)
-        sweep.append((round(eps, 5), r, ix.last_search_kernel_ms()))
-        log("eps %.4f recall@%d %.4f kernel %.2f ms" % (eps, K, r, sweep[-1][2]))
+        r = recall_at(result["ids"].cpu().numpy()[:nq], gt[:nq], K)
+        sweep.append((round(eps, 5), r, ix.last_search_kernel_ms(), nq))
+        log("eps %.4f recall@%d %.4f kernel %.2f ms (%d queries)" % (eps, K, r, sweep[-1][2], nq))
         return r
 
     chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None,
-                          last_ms=lambda: sweep[-1][2])
-    rec = measure(chosen)
+                          last_ms=lambda: sweep[-1][2] * NQ / max(1, sweep[-1][3]))
+    rec = measure(chosen, NQ)
+    for _ in range(20):
+        if rec >= args.target or args.eps:
+            break
+        chosen = round(chosen * 1.02 + 1e-4, 5)
+        rec = measure(chosen, NQ)
     if dist is not None and not shard:
         # replicas: all ranks use the largest epsilon any rank needed
         t = torch.tensor([chosen], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         chosen = float(t.item())
-        rec = measure(chosen)
+        rec = measure(chosen, NQ)
 
     for i in range(max(args.warmup, nstreams)):
         run(chosen, i % nstreams)

@@ -155,6 +155,10 @@ int ngt_amd_search(ngt_amd_index *index, const ngt_amd_search_params *params,
 int ngt_amd_tree_seeds_device(ngt_amd_index *index, const void *d_queries, uint64_t query_bytes, uint32_t nq,
                               uint32_t k, uint32_t *d_seeds, uint32_t seed_stride, uint32_t *d_count,
                               void *stream);
+/* The form of the latest graph-search launch on this index: -1 the
+ * one-expansion-per-pop kernel, 0 the lookahead kernel with a wave per query,
+ * 1 the lookahead kernel with eight waves per query (search_la.hip). */
+int ngt_amd_last_search_lookahead(const ngt_amd_index *index);
 int ngt_amd_search_device(ngt_amd_index *index, const ngt_amd_search_params *params,
                           const void *d_queries, uint64_t query_bytes, uint32_t nq,
                           const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,

@@ -97,6 +97,7 @@ struct SearchCtx {
   uint32_t slots = 0;
   uint32_t launch_slots = 0;     // workgroups (resident waves) of the last launch
   bool launch_filtered = false;  // the last graph-search launch read the filter copy
+  int launch_la = -1;            // the last graph-search launch's lookahead form (-1: none)
   uint64_t vis_stride = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the search kernel
   DevBuf<uint8_t> lut;           // NGTQG: [nq][Me*16]

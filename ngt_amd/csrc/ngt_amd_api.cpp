@@ -413,6 +413,35 @@ static int ensure_filter(ngt_amd_index* ix) {
   return 0;
 }
 
+// Which search kernel a launch takes: -1 the one-expansion-per-pop kernel
+// (search_kernels.hip; every metric), 0 / 1 the lookahead kernel
+// (search_la.hip; L2 over float rows of 96/128 elements with the padded
+// adjacency) in its throughput (a wave per query) or latency (eight waves per
+// query: launches of under two queries per CU -- single C-API calls,
+// coalesced batches, construction batches) form.  NGT_AMD_LA=0 turns the
+// lookahead kernel off, =1 keeps only the throughput form (for any list
+// length), =2 only latency.
+static int lookahead_mode(const ngt_amd_index* ix, const SearchArgs& a, const ngt_amd_search_params* prm,
+                          uint32_t nq) {
+  const char* ev = getenv("NGT_AMD_LA");
+  const int env = ev ? atoi(ev) : 3;
+  if (env == 0) return -1;
+  if (ix->metric != NGT_AMD_DISTANCE_L2 || ix->otype != NGT_AMD_OBJECT_FLOAT || (ix->dp != 128 && ix->dp != 96))
+    return -1;
+  if (!a.adj || a.adj_stride > 256) return -1;
+  if (prm->distance_filter < 0) return -1;  // the lookahead kernel always filters
+  if (getenv("NGT_AMD_FILTER") && atoi(getenv("NGT_AMD_FILTER")) == 0) return -1;
+  const int mode = nq < 2u * (uint32_t)ix->cu_count ? 1 : 0;
+  // a wave per query pays off on short lists (an NGT index at its
+  // EdgeSizeForSearch of 40: ~4 lists per step); long lists (the C2 kNN graph,
+  // ~136 ids) fill a step with one list, and the one-expansion kernel's
+  // chunk pipeline with 16 waves per CU is faster there
+  const uint64_t deg = std::min<uint64_t>(a.adj_stride, a.edge_size);
+  if (mode == 0 && deg > 64 && env != 1) return -1;
+  if ((env & (1 << mode)) == 0) return -1;
+  return mode;
+}
+
 static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_params* prm, const void* d_queries,
                       uint64_t query_bytes, uint32_t nq, const uint32_t* d_seeds,
                       const uint64_t* d_seed_off, uint32_t* d_ids, float* d_dists, uint32_t* d_n,
@@ -440,6 +469,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   }
   if (const char* v = getenv("NGT_AMD_ADJ"))
     if (atoi(v) == 0) a.adj = nullptr;
+  int la_mode = -1;
   a.queries = static_cast<const uint8_t*>(d_queries);
   a.query_bytes = query_bytes;
   a.nq = nq;
@@ -532,13 +562,32 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     const bool want = force >= 0 ? force != 0
                                  : (prm->distance_filter != 0 ? prm->distance_filter > 0
                                                               : nq >= 2u * (uint32_t)ix->cu_count);
-    if (shape && want) {
+    // the lookahead kernel (search_la.hip) shares one filter round trip
+    // among a step's expansions, so it takes the filter at every launch size
+    la_mode = lookahead_mode(ix, a, prm, nq);
+    if (shape && (want || la_mode >= 0)) {
       if (ensure_filter(ix)) return -1;
       a.fcodes = ix->filt.codes.p;
       a.fstride = ix->filt.stride;
       a.fparams = ix->filt.params.p;
     }
     c->launch_filtered = a.fcodes != nullptr;
+    if (!a.fcodes) la_mode = -1;
+  }
+  if (la_mode >= 0) {
+    // one step's target lists (<= 256 ids each) and the exact per-step id set
+    static const uint32_t env_lmax = [] {
+      const char* v = getenv("NGT_AMD_LA_LMAX");
+      return v ? (uint32_t)std::max(256, std::min(8192, atoi(v))) : 0u;
+    }();
+    a.la_lmax = env_lmax ? env_lmax : (la_mode == 0 ? 256u : 2048u);
+    a.la_sh_log2 = 1;
+    while ((1u << a.la_sh_log2) < 2u * a.la_lmax) a.la_sh_log2++;
+    if (a.vf_log2 == 0) a.vf_log2 = 15;
+    a.cq_cap = la_mode == 0 ? 512u : 2048u;
+    if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+    if (const char* v = getenv("NGT_AMD_VFILTER"))
+      if (atoi(v) > 0) a.vf_log2 = (uint32_t)std::max(11, std::min(18, atoi(v)));
   }
 
   if (prm->seed_mode == NGT_AMD_SEED_TREE) {
@@ -551,8 +600,9 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     a.seeds = d_seeds;
     a.seed_off = d_seed_off;
   }
-  const size_t lds = search_lds_bytes(a, ix->otype);
   const size_t lds_max = std::max<size_t>(64 * 1024, std::min<size_t>(ix->lds_per_block, ix->lds_per_cu));
+  if (la_mode >= 0 && search_la_lds_bytes(a, (int)la_targets(la_mode)) > lds_max) la_mode = -1;  // large k
+  const size_t lds = la_mode >= 0 ? search_la_lds_bytes(a, (int)la_targets(la_mode)) : search_lds_bytes(a, ix->otype);
   if (lds > lds_max) return fail("search: k=%u needs %zu bytes of LDS per query (max %zu)", a.k, lds, lds_max);
   if (ensure_vis_scratch(ix, c, lds, nq, s)) return -1;
   a.vis = c->vis.p;
@@ -564,8 +614,14 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   HIP_OK(hipMemsetAsync(c->work.p, 0, sizeof(uint32_t), s));
   uint32_t slots = std::min<uint32_t>(c->slots, nq);
   c->launch_slots = slots;
+  c->launch_la = la_mode;
   HIP_OK(hipEventRecord(c->ev0, s));
-  HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
+  if (la_mode >= 0) {
+    // full visited set unless the caller asked for the accepted-only one
+    HIP_OK(launch_graph_search_la(a, la_mode, !a.accepted_only, slots, s));
+  } else {
+    HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
+  }
   HIP_OK(hipEventRecord(c->ev1, s));
   return 0;
 }
@@ -668,6 +724,12 @@ extern "C" int ngt_amd_last_search_filtered(const ngt_amd_index* ix) {
   if (!ix) return 0;
   SearchCtx* c = ix->last_ctx.load();
   return c && c->launch_filtered ? 1 : 0;
+}
+
+extern "C" int ngt_amd_last_search_lookahead(const ngt_amd_index* ix) {
+  if (!ix) return -1;
+  SearchCtx* c = ix->last_ctx.load();
+  return c ? c->launch_la : -1;
 }
 
 extern "C" uint32_t ngt_amd_last_search_slots(const ngt_amd_index* ix) {

@@ -87,7 +87,17 @@ struct SearchArgs {
   uint64_t* spill;               // [slots][spill_cap]
   uint32_t spill_cap;
   int* error;
+  // lookahead kernel (search_la.hip): list capacity (entries of one step's
+  // target lists, >= 256) and log2 of the per-step id hash (>= log2(2 lmax))
+  uint32_t la_lmax;
+  uint32_t la_sh_log2;
 };
+
+// lookahead targets per step of search_la.hip: mode 0 (throughput, one wave
+// per query), mode 1 (latency, eight waves per query)
+inline uint32_t la_targets(int mode) { return mode == 0 ? 4u : 8u; }
+uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
+hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint32_t slots, hipStream_t s);
 
 struct LinearArgs {
   const uint8_t* rows;

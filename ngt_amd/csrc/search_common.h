@@ -70,6 +70,17 @@ __device__ __forceinline__ void eval_batch(const T* qlds, const uint8_t* rows, u
   }
 }
 
+// One adjacency row of the padded fixed-stride copy, all chunks in one round
+// trip: lane l holds ids l, l + 64, l + 128, l + 192 (0 past `deg`).
+__device__ __forceinline__ void load_adj_row(const uint32_t* row, uint64_t deg, uint32_t& r0, uint32_t& r1,
+                                             uint32_t& r2, uint32_t& r3) {
+  const uint32_t l = (uint32_t)lane_id();
+  r0 = l < deg ? row[l] : 0u;
+  r1 = l + 64 < deg ? row[l + 64] : 0u;
+  r2 = l + 128 < deg ? row[l + 128] : 0u;
+  r3 = l + 192 < deg ? row[l + 192] : 0u;
+}
+
 // ---------------------------------------------------------------------------
 // Graph search.
 // ---------------------------------------------------------------------------

@@ -174,17 +174,6 @@ __device__ __forceinline__ void cq_chunk_min(const uint64_t* cq, uint64_t* cmin,
   if (lane_id() == 0) cmin[c] = m;
 }
 
-// One adjacency row of the padded fixed-stride copy, all chunks in one round
-// trip: lane l holds ids l, l + 64, l + 128, l + 192 (0 past `deg`).
-__device__ __forceinline__ void load_adj_row(const uint32_t* row, uint64_t deg, uint32_t& r0, uint32_t& r1,
-                                             uint32_t& r2, uint32_t& r3) {
-  const uint32_t l = (uint32_t)lane_id();
-  r0 = l < deg ? row[l] : 0u;
-  r1 = l + 64 < deg ? row[l + 64] : 0u;
-  r2 = l + 128 < deg ? row[l + 128] : 0u;
-  r3 = l + 192 < deg ? row[l + 192] : 0u;
-}
-
 template <int M, typename T, int NCH, int G>
 __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -1,0 +1,785 @@
+// search_la.hip -- the best-first search of NeighborhoodGraph::searchReadOnlyGraph
+// (lib/NGT/Graph.cpp:398-495) with LOOKAHEAD: one step expands the node the
+// reference pops next together with the next P-1 keys of the unchecked set, so
+// a step's memory round trips (adjacency rows, filter codes + visited probes,
+// exact rows) serve up to P expansions instead of one.
+//
+// Shape: L2 over float rows of dp = 16 * NCH (96 / 128 elements) with the
+// 1-byte filter copy (filter_kernels.hip, bound in search_common.h) and the
+// padded adjacency (each list's first min(degree, edgeSize) ids, <= 256).
+//
+// Why the traversal is the reference's:
+//  * the distances of a node's neighbours do not depend on the search state,
+//    so computing them before the node is popped changes nothing; only the
+//    ACCEPT step (Graph.cpp:462-483) is order-dependent, and it runs strictly in
+//    the reference's pop order ("commit"): target j > 0 is committed only if
+//    it is exactly the key the reference pops next (minimum of the unchecked
+//    set, LDS + spill, within the exploration radius); otherwise the rest of
+//    the step's speculation is discarded and the next step pops normally;
+//  * the filter threshold of a step comes from the exploration radius at the
+//    step's start; the radius only shrinks, so a neighbour the bound rejects
+//    is also outside the radius when it is committed;
+//  * "fresh" (not visited) is decided at the step's start from the visited set
+//    (LDS filter bits + HBM epoch bytes); ids marked by this step's earlier
+//    commits are caught at commit time by an exact per-step LDS hash.
+//  FULL = every evaluated id is marked (the reference's visited set and its
+//  distance-computation count); !FULL = the accepted-only set of
+//  search_common.h (not_accepted): identical results, re-evaluations counted.
+//
+// Workgroup = W waves serve one query (W = 1: throughput launches, a wave per
+// query per SIMD slot; W = 8: latency launches -- single C-API queries, small
+// batches -- where a lone query gets a CU's worth of loads in flight).  Wave 0
+// owns the sequential state (unchecked keys, results, radius); every wave
+// shares the gathers.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ngt_device.h"
+#include "ngt_kernels.h"
+#include "search_common.h"
+
+namespace ngt_amd {
+
+struct LaCtl {
+  uint32_t qi, done, nt, ntl, nl, nx, fthr, fsq;
+  uint32_t epoch, pad[7];
+};
+
+// 16-byte aligned LDS carve-out; the host's search_la_lds_bytes mirrors it.
+struct LaLayout {
+  uint32_t off_tkey, off_tcnt, off_loff, off_xoff, off_vf, off_cq, off_cmin, off_res, off_q, off_qb, off_l,
+      off_lfl, off_x, off_xd, off_sh, off_nid, off_nd, total;
+  __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
+  __host__ __device__ LaLayout(const SearchArgs& a, int P) {
+    uint32_t o = up16(sizeof(LaCtl));
+    off_tkey = o; o = up16(o + 8u * P);
+    off_tcnt = o; o = up16(o + 4u * P);
+    off_loff = o; o = up16(o + 4u * (P + 1));
+    off_xoff = o; o = up16(o + 4u * (P + 1));
+    off_vf = o; o = up16(o + ((1u << a.vf_log2) >> 3));
+    off_cq = o; o = up16(o + 8u * a.cq_cap);
+    off_cmin = o; o = up16(o + 8u * ((a.cq_cap + 63) / 64));
+    off_res = o; o = up16(o + 8u * (a.k + 1));
+    off_q = o; o = up16(o + 4u * (uint32_t)a.dp);
+    off_qb = o; o = up16(o + (uint32_t)a.dp);
+    off_l = o; o = up16(o + 4u * a.la_lmax);
+    off_lfl = o; o = up16(o + a.la_lmax);
+    off_x = o; o = up16(o + 4u * a.la_lmax);
+    off_xd = o; o = up16(o + 4u * a.la_lmax);
+    off_sh = o; o = up16(o + (4u << a.la_sh_log2));
+    off_nid = o; o = up16(o + 256u);
+    off_nd = o; o = up16(o + 256u);
+    total = o;
+  }
+};
+
+// exact per-step set of ids (open addressing, 0 = empty)
+__device__ __forceinline__ uint32_t sh_slot(uint32_t id, uint32_t log2) { return (id * 0x9E3779B1u) >> (32 - log2); }
+__device__ __forceinline__ bool sh_contains(const uint32_t* sh, uint32_t log2, uint32_t id) {
+  const uint32_t mask = (1u << log2) - 1u;
+  for (uint32_t h = sh_slot(id, log2);; h = (h + 1) & mask) {
+    const uint32_t v = sh[h];
+    if (v == id) return true;
+    if (v == 0u) return false;
+  }
+}
+__device__ __forceinline__ void sh_insert(uint32_t* sh, uint32_t log2, uint32_t id) {
+  const uint32_t mask = (1u << log2) - 1u;
+  for (uint32_t h = sh_slot(id, log2);; h = (h + 1) & mask) {
+    const uint32_t old = atomicCAS(sh + h, 0u, id);
+    if (old == 0u || old == id) return;
+  }
+}
+
+__device__ __forceinline__ void vf_set(uint32_t* vf, uint32_t shift, uint32_t id) {
+  const uint32_t b = (id * 0x85EBCA77u) >> shift;
+  atomicOr(vf + (b >> 5), 1u << (b & 31));
+}
+__device__ __forceinline__ bool vf_test(const uint32_t* vf, uint32_t shift, uint32_t id) {
+  const uint32_t b = (id * 0x85EBCA77u) >> shift;
+  return (vf[b >> 5] >> (b & 31)) & 1u;
+}
+
+// W = 1: three waves per SIMD (<= 168 VGPRs; the LDS allows ~10 waves per CU)
+template <int NCH, int W, int PW, int RG, int EG, bool FULL>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 3 : 2)))
+ngt_graph_search_la_kernel(SearchArgs a) {
+  constexpr int P = W * PW;
+  constexpr int E = 4 * NCH;  // filter-code bytes per lane of a quad
+  constexpr int NW = E / 8;   // 8-byte code words per lane
+  static_assert((NCH & 1) == 0, "whole 8-byte code words per lane");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const LaLayout lay(a, P);
+  LaCtl* ctl = reinterpret_cast<LaCtl*>(smem);
+  uint64_t* tkey = reinterpret_cast<uint64_t*>(smem + lay.off_tkey);
+  uint32_t* tcnt = reinterpret_cast<uint32_t*>(smem + lay.off_tcnt);
+  uint32_t* loff = reinterpret_cast<uint32_t*>(smem + lay.off_loff);
+  uint32_t* xoff = reinterpret_cast<uint32_t*>(smem + lay.off_xoff);
+  uint32_t* vf = reinterpret_cast<uint32_t*>(smem + lay.off_vf);
+  uint64_t* cq = reinterpret_cast<uint64_t*>(smem + lay.off_cq);
+  uint64_t* cmin = reinterpret_cast<uint64_t*>(smem + lay.off_cmin);
+  uint64_t* res = reinterpret_cast<uint64_t*>(smem + lay.off_res);
+  float* qlds = reinterpret_cast<float*>(smem + lay.off_q);
+  uint8_t* qb = smem + lay.off_qb;
+  uint32_t* L = reinterpret_cast<uint32_t*>(smem + lay.off_l);
+  uint8_t* lfl = smem + lay.off_lfl;
+  uint32_t* X = reinterpret_cast<uint32_t*>(smem + lay.off_x);
+  float* Xd = reinterpret_cast<float*>(smem + lay.off_xd);
+  uint32_t* sh = reinterpret_cast<uint32_t*>(smem + lay.off_sh);
+  uint32_t* nid = reinterpret_cast<uint32_t*>(smem + lay.off_nid);
+  float* nd = reinterpret_cast<float*>(smem + lay.off_nd);
+
+  const int lane = lane_id();
+  const int wave = (int)(threadIdx.x >> 6);
+  const uint32_t tid = threadIdx.x;
+  constexpr uint32_t NT = 64u * W;
+  const uint32_t vf_words = (1u << a.vf_log2) / 32;
+  const uint32_t vf_shift = 32 - a.vf_log2;
+  const uint32_t sh_n = 1u << a.la_sh_log2;
+  const uint32_t lmax = a.la_lmax;
+  const float fa = a.fparams[0], fb = a.fparams[1], fe = a.fparams[2];
+  const double finv_b = 1.0 / (double)fb;
+  const uint32_t slot = blockIdx.x;
+  uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
+  uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
+  const uint64_t deg_cap = a.adj_stride < a.edge_size ? a.adj_stride : a.edge_size;
+  const uint32_t k = a.k;
+  const int g = lane & 3, rs = lane >> 2;
+
+  for (;;) {
+    if (tid == 0) ctl->qi = atomicAdd(a.work, 1u);
+    __syncthreads();
+    const uint32_t qi = ctl->qi;
+    if (qi >= a.nq) break;
+
+    // ---- per-query init (every wave) -------------------------------------
+    for (uint32_t i = tid; i < vf_words; i += NT) vf[i] = 0u;
+    {
+      const uint4* s = reinterpret_cast<const uint4*>(a.queries + (uint64_t)qi * a.query_bytes);
+      uint4* d = reinterpret_cast<uint4*>(qlds);
+      for (uint32_t i = tid; i < (uint32_t)a.dp / 4; i += NT) d[i] = s[i];
+    }
+    uint32_t epoch = a.slot_epoch[slot] + 1;
+    if (epoch > 255) {
+      uint4* v4 = reinterpret_cast<uint4*>(vis);
+      for (uint64_t i = tid; i < a.vis_stride / 16; i += NT) v4[i] = make_uint4(0, 0, 0, 0);
+      epoch = 1;
+    }
+    __syncthreads();
+    if (tid == 0) a.slot_epoch[slot] = epoch;
+
+    // wave 0's sequential state
+    uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
+    uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, ndisc = 0, ns = 0;
+    float radius = a.radius;
+    float expr = 0.f;
+    double frq = 0.0;
+    // ---- the unchecked set: two levels with a key threshold T ------------
+    // LDS keys are all < T <= every spill key (HBM, per slot), so the
+    // minimum is always in LDS while LDS is non-empty (chunk minima, no
+    // spill scan).  A full LDS is compacted (keys beyond the exploration
+    // radius can never be popped, Graph.cpp:433-435) and, if still over
+    // half full, its larger half moves to the spill (T drops); an empty LDS
+    // refills with the smallest spill keys (T rises).  Exact throughout.
+    uint64_t T = ~0ull;
+    auto chunk_min = [&](uint32_t c) {
+      const uint32_t i = 64 * c + (uint32_t)lane;
+      const uint64_t mn = wave_min_u64(i < ncq ? cq[i] : ~0ull);
+      if (lane == 0) cmin[c] = mn;
+    };
+    auto all_chunk_min = [&]() {
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t c = 0; c < ((ncq + 63) >> 6); c++) chunk_min(c);
+      __builtin_amdgcn_wave_barrier();
+    };
+    auto spill_push = [&](uint64_t key) {
+      if (nspill >= a.spill_cap) {
+        if (lane == 0) atomicOr(a.error, 1);
+      } else {
+        if (lane == 0) spill[nspill] = key;
+        nspill++;
+      }
+    };
+    // move the LDS keys >= t to the spill (t lowers T)
+    auto lds_to_spill = [&](uint64_t t) {
+      uint32_t out = 0;
+      for (uint32_t b = 0; b < ncq; b += 64) {
+        const uint32_t i = b + (uint32_t)lane;
+        const uint64_t key = i < ncq ? cq[i] : ~0ull;
+        const bool mv = i < ncq && key >= t;
+        const bool keep = i < ncq && key < t;
+        const uint64_t mm = ballot64(mv), km = ballot64(keep);
+        const uint32_t nm = (uint32_t)__popcll(mm);
+        if (nspill + nm > a.spill_cap) {
+          if (lane == 0) atomicOr(a.error, 1);
+        } else if (mv) {
+          spill[nspill + mbcnt(mm)] = key;
+        }
+        if (nspill + nm <= a.spill_cap) nspill += nm;
+        __builtin_amdgcn_wave_barrier();
+        if (keep) cq[out + mbcnt(km)] = key;
+        __builtin_amdgcn_wave_barrier();
+        out += (uint32_t)__popcll(km);
+      }
+      ncq = out;
+      T = t;
+    };
+    auto make_room = [&]() {
+      ncq = compact(cq, ncq, expr);
+      const uint32_t keep = a.cq_cap / 2;
+      if (ncq > keep) {
+        // bisect for the threshold t that keeps between keep/2 and keep keys
+        uint64_t lo = ~0ull, hi = 0;
+        for (uint32_t i = lane; i < ncq; i += 64) {
+          const uint64_t v = cq[i];
+          lo = v < lo ? v : lo;
+          hi = v > hi ? v : hi;
+        }
+        lo = wave_min_u64(lo);
+        hi = ~wave_min_u64(~hi);  // max
+        // the largest t with count(keys < t) <= keep (keys are distinct, so
+        // the count rises by one per key): l is always such a t
+        uint64_t l = lo, h = hi;
+        for (int it = 0; it < 64 && l < h; it++) {
+          const uint64_t mid = l + ((h - l) >> 1) + 1;
+          uint32_t c = 0;
+          for (uint32_t i = lane; i < ncq; i += 64) c += cq[i] < mid ? 1u : 0u;
+          c = wave_sum_u32(c);
+          if (c <= keep) {
+            l = mid;
+            if (c >= keep / 2) break;
+          } else {
+            h = mid - 1;
+          }
+        }
+        lds_to_spill(l);
+      }
+      all_chunk_min();
+    };
+    // refill an empty LDS with the smallest spill keys within the radius
+    auto refill = [&]() {
+      const uint32_t want = a.cq_cap / 2;
+      uint32_t* hist = nid;  // 64 counters (free outside the accept staging)
+      // key distances as ordered 32-bit values; the spill keys within the radius
+      const uint32_t lim = ord_of(expr);
+      uint32_t lo = 0xffffffffu, hi = 0;
+      for (uint32_t i = lane; i < nspill; i += 64) {
+        const uint32_t o = (uint32_t)(spill[i] >> 32);
+        if (o <= lim) {
+          lo = o < lo ? o : lo;
+          hi = o > hi ? o : hi;
+        }
+      }
+      lo = (uint32_t)(wave_min_u64(lo) & 0xffffffffu);
+      hi = (uint32_t)(~wave_min_u64(~(uint64_t)hi) & 0xffffffffu);
+      uint32_t bound = 0;  // spill keys with ord < bound move to LDS
+      if (lo > hi) {
+        nspill = 0;  // nothing within the radius: the search ends
+        T = ~0ull;
+        return;
+      }
+      for (;;) {
+        const uint64_t span = (uint64_t)hi - lo + 1;
+        const uint64_t width = (span + 63) / 64;
+        hist[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < nspill; i += 64) {
+          const uint32_t o = (uint32_t)(spill[i] >> 32);
+          if (o >= lo && o <= hi) atomicAdd(hist + (uint32_t)(((uint64_t)o - lo) / width), 1u);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // largest b with sum(hist[0..b)) <= want
+        const uint32_t h = hist[lane];
+        uint32_t incl = h;  // inclusive prefix over lanes
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t v = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += v;
+        }
+        const uint64_t okm = ballot64(incl <= want);
+        const uint32_t b = (uint32_t)__popcll(okm);  // bins [0, b) fit (prefix is monotone)
+        if (b >= 1 || width == 1) {
+          bound = b >= 1 ? (uint32_t)std::min<uint64_t>((uint64_t)lo + b * width, 0xffffffffull) : lo + 1;
+          if (b == 0 && lane == 0) atomicOr(a.error, 8);  // > want keys share one distance: never expected
+          break;
+        }
+        hi = (uint32_t)(lo + width - 1);  // the first bin alone is too big: refine it
+      }
+      // move: ord < bound (and within the radius) to LDS; keep ord >= bound
+      // (within the radius) in the spill, compacted in place
+      uint32_t out = 0;
+      for (uint32_t b0 = 0; b0 < nspill; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < nspill ? spill[i] : ~0ull;
+        const uint32_t o = (uint32_t)(key >> 32);
+        const bool in = i < nspill && o <= lim;
+        // (the histogram bounds the moved keys by want <= cq_cap / 2; the
+        // flagged degenerate bound above keeps any excess in the spill)
+        const bool fits = ncq + mbcnt(ballot64(in && o < bound)) < a.cq_cap;
+        const bool mv = in && o < bound && fits;
+        const bool stay = in && !mv;
+        const uint64_t mm = ballot64(mv), sm = ballot64(stay);
+        __builtin_amdgcn_wave_barrier();
+        if (mv) cq[ncq + mbcnt(mm)] = key;
+        if (stay) spill[out + mbcnt(sm)] = key;
+        __builtin_amdgcn_wave_barrier();
+        ncq += (uint32_t)__popcll(mm);
+        out += (uint32_t)__popcll(sm);
+      }
+      nspill = out;
+      T = nspill ? ((uint64_t)bound << 32) : ~0ull;
+      all_chunk_min();
+    };
+    auto insert_key = [&](uint64_t key) {
+      if (key >= T) {
+        spill_push(key);
+      } else {
+        if (ncq >= a.cq_cap) make_room();
+        if (key >= T) {
+          spill_push(key);
+        } else {
+          if (lane == 0) {
+            cq[ncq] = key;
+            const uint32_t c = ncq >> 6;
+            cmin[c] = (ncq & 63) == 0 ? key : (key < cmin[c] ? key : cmin[c]);
+          }
+          ncq++;
+        }
+      }
+      if (ncq + nspill > maxq) maxq = ncq + nspill;
+      __builtin_amdgcn_wave_barrier();
+    };
+    // the minimum of the unchecked set (and its LDS chunk)
+    auto find_min = [&](uint32_t& bidx) -> uint64_t {
+      if (ncq == 0 && nspill != 0) refill();
+      uint64_t best = ~0ull;
+      bidx = 0xffffffffu;
+      const uint32_t nch = (ncq + 63) >> 6;
+      if ((uint32_t)lane < nch) { best = cmin[lane]; bidx = (uint32_t)lane; }
+      if ((uint32_t)lane + 64 < nch) {
+        const uint64_t v = cmin[lane + 64];
+        if (v < best) { best = v; bidx = (uint32_t)lane + 64; }
+      }
+      const uint64_t wbest = wave_min_u64(best);
+      const uint64_t owner = ballot64(best == wbest);
+      bidx = __shfl(bidx, __ffsll((long long)owner) - 1, 64);
+      return wbest;
+    };
+    // remove the minimum found by find_min; false on a stale chunk minimum
+    auto remove_min = [&](uint64_t wbest, uint32_t bidx) -> bool {
+      const uint32_t i = 64 * bidx + (uint32_t)lane;
+      const uint64_t in = ballot64(i < ncq && cq[i] == wbest);
+      if (in == 0) return false;
+      bidx = 64 * bidx + (uint32_t)(__ffsll((long long)in) - 1);
+      if (lane == 0) cq[bidx] = cq[ncq - 1];
+      __builtin_amdgcn_wave_barrier();
+      ncq--;
+      const uint32_t c0 = bidx >> 6, c1 = ncq >> 6;
+      chunk_min(c0);
+      if (c1 != c0) chunk_min(c1);
+      __builtin_amdgcn_wave_barrier();
+      return true;
+    };
+    // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
+    // order (Graph.cpp:471-483); only candidates within the radius at batch
+    // start can be accepted
+    auto accept = [&](uint32_t me) {
+      uint64_t okmask = ballot64((uint32_t)lane < me && nd[lane] <= expr);
+      while (okmask) {
+        const int j = __ffsll((long long)okmask) - 1;
+        okmask &= okmask - 1;
+        const float d = nd[j];
+        if (!(d <= expr)) continue;
+        const uint32_t id = nid[j];
+        const uint64_t key = make_key(d, id);
+        if constexpr (!FULL) {
+          if (lane == 0) {
+            vf_set(vf, vf_shift, id);
+            vis[id] = (uint8_t)epoch;
+            sh_insert(sh, a.la_sh_log2, id);
+          }
+        }
+        insert_key(key);
+        if (d <= radius) {
+          res_insert(res, nres, k, key);
+          if (nres >= k) {
+            radius = key_dist(res[k - 1]);
+            expr = __fmul_rn(a.coef, radius);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    };
+
+    if (wave == 0) {
+      uint32_t fsq = 0;
+      filter_query(qlds, a.dp, fa, fb, qb, fsq, frq);
+      if (lane == 0) ctl->fsq = fsq;
+      // ---- setupDistances + setupSeeds (Graph.cpp:293-367) --------------
+      const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
+      ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
+      for (uint32_t base = 0; base < ns; base += 64) {
+        const uint32_t m = ns - base < 64 ? (uint32_t)(ns - base) : 64u;
+        if ((uint32_t)lane < m) nid[lane] = a.seeds[sb + base + lane];
+        __builtin_amdgcn_wave_barrier();
+        eval_l2f_fast<NCH, 1>(qlds, a.rows, a.row_bytes, nid, nd, (int)m);
+        __builtin_amdgcn_wave_barrier();
+        if ((uint32_t)lane < m) {
+          const uint32_t id = nid[lane];
+          vf_set(vf, vf_shift, id);
+          vis[id] = (uint8_t)epoch;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // every seed enters the unchecked set (Graph.cpp:355-366), the first
+        // k within the radius the results
+        for (uint32_t j = 0; j < m; j++) {
+          const float d = nd[j];
+          const uint64_t key = make_key(d, nid[j]);
+          insert_key(key);
+          if (d <= a.radius) res_insert(res, nres, k, key);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      ndist = ns;
+      if (nres >= k) radius = key_dist(res[k - 1]);
+      expr = __fmul_rn(a.coef, radius);
+    }
+
+    // ---- best-first loop (Graph.cpp:430-486), P expansions per step --------
+    for (;;) {
+      // A. wave 0: pop the reference's next node, pick the next keys in line
+      if (wave == 0) {
+        uint32_t bidx;
+        const uint64_t key = find_min(bidx);
+        uint32_t done = 0, nt = 0;
+        if (key == ~0ull || key_dist(key) > expr) {
+          done = 1;
+        } else if (!remove_min(key, bidx)) {
+          if (lane == 0) atomicOr(a.error, 4);  // stale chunk minimum: never expected
+          done = 1;
+        } else {
+          if (lane == 0) tkey[0] = key;
+          nt = 1;
+          uint64_t prev = key;
+          for (int j = 1; j < P; j++) {
+            uint64_t m = ~0ull;
+            for (uint32_t i = lane; i < ncq; i += 64) {
+              const uint64_t v = cq[i];
+              if (v > prev && v < m) m = v;
+            }
+            m = wave_min_u64(m);
+            if (m == ~0ull || key_dist(m) > expr) break;
+            if (lane == 0) tkey[j] = m;
+            prev = m;
+            nt++;
+          }
+        }
+        if (lane == 0) {
+          ctl->done = done;
+          ctl->nt = nt;
+          ctl->fthr = filter_threshold(expr, (double)fe, finv_b, frq);
+        }
+      }
+      __syncthreads();
+      if (ctl->done) break;
+      const uint32_t nt = ctl->nt;
+
+      // B. adjacency rows of the targets (target j on wave j mod W), one round trip
+      uint32_t r[PW][4];
+      uint32_t cnt[PW];
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) {
+        const uint32_t j = (uint32_t)(wave + W * jj);
+        cnt[jj] = 0;
+        if (j < nt) load_adj_row(a.adj + (uint64_t)key_id(tkey[j]) * a.adj_stride, deg_cap, r[jj][0], r[jj][1],
+                                 r[jj][2], r[jj][3]);
+        else r[jj][0] = r[jj][1] = r[jj][2] = r[jj][3] = 0u;
+      }
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) {
+        const uint32_t j = (uint32_t)(wave + W * jj);
+        // 0-terminated rows: the ids form a prefix
+        cnt[jj] = (uint32_t)(__popcll(ballot64(r[jj][0] != 0u)) + __popcll(ballot64(r[jj][1] != 0u)) +
+                             __popcll(ballot64(r[jj][2] != 0u)) + __popcll(ballot64(r[jj][3] != 0u)));
+        if (j < nt && lane == 0) tcnt[j] = cnt[jj];
+      }
+      // the step hash starts empty
+      for (uint32_t i = tid; i < sh_n; i += NT) sh[i] = 0u;
+      __syncthreads();
+      // list offsets: the targets whose lists fit the list capacity (t0 always does)
+      uint32_t ntl = nt, tot = 0;
+      uint32_t myoff[PW];
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) myoff[jj] = 0xffffffffu;
+      for (uint32_t j = 0; j < nt; j++) {
+        const uint32_t c = tcnt[j];
+        if (tot + c > lmax) { ntl = j; break; }
+#pragma unroll
+        for (int jj = 0; jj < PW; jj++)
+          if (j == (uint32_t)(wave + W * jj)) myoff[jj] = tot;
+        if (tid == 0) loff[j] = tot;
+        tot += c;
+      }
+      if (tid == 0) {
+        loff[ntl] = tot;
+        ctl->ntl = ntl;
+        ctl->nl = tot;
+      }
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) {
+        if (myoff[jj] == 0xffffffffu) continue;
+        const uint32_t o = myoff[jj], c = cnt[jj];
+        if ((uint32_t)lane < c) L[o + lane] = r[jj][0];
+        if ((uint32_t)lane + 64 < c) L[o + 64 + lane] = r[jj][1];
+        if ((uint32_t)lane + 128 < c) L[o + 128 + lane] = r[jj][2];
+        if ((uint32_t)lane + 192 < c) L[o + 192 + lane] = r[jj][3];
+      }
+      __syncthreads();
+      const uint32_t nl = tot;
+
+      // C. visited-at-step-start test + filter codes of every list entry:
+      // quad per entry, RG groups of 16 entries in flight per wave
+      {
+        const uint32_t fthr = ctl->fthr, fsq = ctl->fsq;
+        uint2 q[NW];
+        const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
+#pragma unroll
+        for (int w = 0; w < NW; w++) q[w] = qp[w];
+        for (uint32_t base = (uint32_t)wave * 16u * RG; base < nl; base += 16u * RG * W) {
+          uint2 c[RG][NW];
+          uint32_t ids[RG], pw[RG];
+          bool bit[RG];
+#pragma unroll
+          for (int j = 0; j < RG; j++) {
+            const uint32_t e = base + 16u * j + (uint32_t)rs;
+            const uint32_t id = e < nl ? L[e] : 0u;
+            ids[j] = id;
+            bit[j] = id != 0u && vf_test(vf, vf_shift, id);
+            pw[j] = 0u;
+            if (bit[j] && g == 0)
+              pw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+            const uint2* cp = reinterpret_cast<const uint2*>(a.fcodes + (uint64_t)id * (4 * E)) + g * NW;
+            if (base + 16u * j < nl) {
+#pragma unroll
+              for (int w = 0; w < NW; w++) c[j][w] = cp[w];
+            } else {
+#pragma unroll
+              for (int w = 0; w < NW; w++) c[j][w] = make_uint2(0u, 0u);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < RG; j++) {
+            if (base + 16u * j >= nl) continue;
+            uint32_t qc = 0u, cc = 0u;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+              qc = __builtin_amdgcn_udot4(q[w].x, c[j][w].x, qc, false);
+              qc = __builtin_amdgcn_udot4(q[w].y, c[j][w].y, qc, false);
+              cc = __builtin_amdgcn_udot4(c[j][w].x, c[j][w].x, cc, false);
+              cc = __builtin_amdgcn_udot4(c[j][w].y, c[j][w].y, cc, false);
+            }
+            const uint32_t S = fsq + quad_sum_u32(cc - 2u * qc);
+            const uint32_t e = base + 16u * j + (uint32_t)rs;
+            const uint32_t id = ids[j];
+            if (g == 0 && e < nl) {
+              const bool fresh = !bit[j] || ((pw[j] >> (8 * (id & 3))) & 0xffu) != epoch;
+              lfl[e] = (uint8_t)((fresh ? 1u : 0u) | (fresh && S <= fthr ? 2u : 0u));
+            }
+          }
+        }
+      }
+      __syncthreads();
+
+      // D. survivors (keep bits) of every target, in target then neighbour order
+      const uint32_t ntl_s = ctl->ntl;
+      uint32_t xc[PW];
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) {
+        const uint32_t j = (uint32_t)(wave + W * jj);
+        xc[jj] = 0;
+        if (j >= ntl_s) continue;
+        const uint32_t lb = loff[j], le = loff[j + 1];
+        for (uint32_t e0 = lb; e0 < le; e0 += 64) {
+          const uint32_t e = e0 + (uint32_t)lane;
+          xc[jj] += (uint32_t)__popcll(ballot64(e < le && (lfl[e] & 2u)));
+        }
+        if (lane == 0) xoff[j] = xc[jj];  // count; prefix below
+      }
+      __syncthreads();
+      uint32_t xo[PW], xtot = 0;
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) xo[jj] = 0;
+      for (uint32_t j = 0; j < ntl_s; j++) {
+        const uint32_t c = xoff[j];
+#pragma unroll
+        for (int jj = 0; jj < PW; jj++)
+          if (j == (uint32_t)(wave + W * jj)) xo[jj] = xtot;
+        xtot += c;
+      }
+      __syncthreads();  // every wave has read the counts
+#pragma unroll
+      for (int jj = 0; jj < PW; jj++) {
+        const uint32_t j = (uint32_t)(wave + W * jj);
+        if (j >= ntl_s) continue;
+        if (lane == 0) xoff[j] = xo[jj];
+        const uint32_t lb = loff[j], le = loff[j + 1];
+        uint32_t o = xo[jj];
+        for (uint32_t e0 = lb; e0 < le; e0 += 64) {
+          const uint32_t e = e0 + (uint32_t)lane;
+          const bool kp = e < le && (lfl[e] & 2u);
+          const uint64_t km = ballot64(kp);
+          if (kp) X[o + mbcnt(km)] = L[e];
+          o += (uint32_t)__popcll(km);
+        }
+      }
+      __syncthreads();
+
+      // E. exact comparator distances of the survivors (bit-identical to
+      // PrimitiveComparator::compareL2 through l2_fold_rows)
+      {
+        const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
+        for (uint32_t r0 = (uint32_t)wave * 16u * EG; r0 < xtot; r0 += 16u * EG * W) {
+          float4 v[EG][NCH];
+#pragma unroll
+          for (int j = 0; j < EG; j++) {
+            const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
+            const uint32_t id = rr < xtot ? X[rr] : 0u;
+            const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)id * a.row_bytes) + g;
+            if (j == 0 || r0 + 16u * j < xtot) {
+#pragma unroll
+              for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < EG; j++) {
+            if (j != 0 && r0 + 16u * j >= xtot) continue;
+            const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
+            const float d = l2_fold_rows<NCH>(qq, v[j]);
+            if (g == 0 && rr < xtot) Xd[rr] = d;
+          }
+        }
+      }
+      __syncthreads();
+
+      // F. wave 0 commits in the reference's pop order
+      if (wave == 0) {
+        uint32_t done = 0;
+        for (uint32_t j = 0; j < ntl_s; j++) {
+          if (j > 0) {
+            uint32_t bidx;
+            const uint64_t m = find_min(bidx);
+            if (m == ~0ull || key_dist(m) > expr) {  // the reference stops here (Graph.cpp:433-435)
+              done = 1;
+              ndisc += ntl_s - j;
+              break;
+            }
+            if (m != tkey[j]) {  // something closer was accepted: speculation ends
+              ndisc += ntl_s - j;
+              break;
+            }
+            if (!remove_min(m, bidx)) {
+              if (lane == 0) atomicOr(a.error, 4);
+              done = 1;
+              break;
+            }
+          }
+          nexp++;
+          const uint32_t lb = loff[j], le = loff[j + 1];
+          nedge += le - lb;
+          uint32_t xr = xoff[j];
+          for (uint32_t e0 = lb; e0 < le; e0 += 64) {
+            const uint32_t e = e0 + (uint32_t)lane;
+            const bool in = e < le;
+            const uint32_t id = in ? L[e] : 0u;
+            const uint32_t fl = in ? lfl[e] : 0u;
+            const uint64_t kmask = ballot64((fl & 2u) != 0u);  // positions in X
+            const uint32_t xi = xr + mbcnt(kmask);
+            xr += (uint32_t)__popcll(kmask);
+            const bool fresh = (fl & 1u) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
+            if constexpr (FULL) {
+              if (fresh) {
+                vf_set(vf, vf_shift, id);
+                vis[id] = (uint8_t)epoch;
+                sh_insert(sh, a.la_sh_log2, id);
+              }
+            }
+            ndist += (uint32_t)__popcll(ballot64(fresh));
+            const bool keep = fresh && (fl & 2u);
+            const uint64_t km = ballot64(keep);
+            if (keep) {
+              nid[mbcnt(km)] = id;
+              nd[mbcnt(km)] = Xd[xi];
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t me = (uint32_t)__popcll(km);
+            nexact += me;
+            if (me) accept(me);
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+        if (lane == 0 && done) ctl->done = 1;
+      }
+      __syncthreads();
+      if (ctl->done) break;
+    }
+
+    // ---- results (moveFrom: ascending (distance, id), ObjectSpace.h:49-57)
+    if (wave == 0) {
+      for (uint32_t i = lane; i < nres; i += 64) {
+        a.out_ids[(uint64_t)qi * k + i] = key_id(res[i]);
+        a.out_dists[(uint64_t)qi * k + i] = key_dist(res[i]);
+      }
+      if (lane == 0) {
+        a.out_n[qi] = nres;
+        if (a.counters) {
+          uint64_t* c = a.counters + (uint64_t)qi * 8;
+          c[0] = ndist;
+          c[1] = ndist - ns;
+          c[2] = nexp;
+          c[3] = ndisc;   // speculative expansions discarded
+          c[4] = nedge;
+          c[5] = maxq;
+          c[6] = nexact;  // exact neighbour distances of the committed expansions
+          c[7] = ns;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+uint32_t search_la_lds_bytes(const SearchArgs& a, int P) { return LaLayout(a, P).total; }
+
+// mode 0: throughput (W = 1), mode 1: latency (W = 8)
+hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint32_t slots, hipStream_t s) {
+  if (a.nq == 0) return hipSuccess;
+  if (a.dp != 128 && a.dp != 96) return hipErrorNotSupported;
+  const uint32_t P = la_targets(mode);
+  const size_t lds = search_la_lds_bytes(a, (int)P);
+#define LA(NCH, W, PW, RG, EG, F)                                                                              \
+  do {                                                                                                          \
+    auto kern = ngt_graph_search_la_kernel<NCH, W, PW, RG, EG, F>;                                              \
+    if (lds > 64 * 1024) {                                                                                       \
+      hipError_t e_ = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      if (e_ != hipSuccess) return e_;                                                                          \
+    }                                                                                                           \
+    hipLaunchKernelGGL(kern, dim3(slots), dim3(64 * W), lds, s, a);                                             \
+  } while (0)
+  if (mode == 0) {
+    if (a.dp == 128) {
+      if (full) LA(8, 1, 4, 6, 1, true); else LA(8, 1, 4, 6, 1, false);
+    } else {
+      if (full) LA(6, 1, 4, 6, 1, true); else LA(6, 1, 4, 6, 1, false);
+    }
+  } else {
+    if (a.dp == 128) {
+      if (full) LA(8, 8, 1, 4, 1, true); else LA(8, 8, 1, 4, 1, false);
+    } else {
+      if (full) LA(6, 8, 1, 4, 1, true); else LA(6, 8, 1, 4, 1, false);
+    }
+  }
+#undef LA
+  return hipGetLastError();
+}
+
+}  // namespace ngt_amd

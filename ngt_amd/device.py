@@ -132,6 +132,11 @@ class DeviceIndex(object):
         [6]: exact neighbour distances, [7]: seed distances)."""
         return bool(self.L.ngt_amd_last_search_filtered(self.h))
 
+    def last_search_lookahead(self):
+        """Form of the latest graph-search launch: -1 one expansion per pop,
+        0 lookahead with a wave per query, 1 lookahead with eight waves per query."""
+        return int(self.L.ngt_amd_last_search_lookahead(self.h))
+
     def last_search_slots(self):
         """Workgroups (resident query slots) of the last search launch."""
         return int(self.L.ngt_amd_last_search_slots(self.h))

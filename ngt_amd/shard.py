@@ -119,6 +119,9 @@ class ShardedIndex(object):
         if stream is None or getattr(self.device, "type", "cpu") != "cuda":
             yield None
             return
+        if int(stream) == self.torch.cuda.current_stream(self.device).cuda_stream:
+            yield None  # already torch's current stream: everything is ordered on it
+            return
         ext = self.torch.cuda.ExternalStream(stream, device=self.device)
         with self.torch.cuda.stream(ext):
             yield ext
