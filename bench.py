@@ -243,6 +243,7 @@ def main():
     ap.add_argument("--qg-edges", type=int, default=128, help="NGTQG max edges per node")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sweep-nq", type=int, default=2000, help="queries per epsilon-sweep launch")
+    ap.add_argument("--latency-queries", type=int, default=100, help="single-query launches timed after the bench")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
     ap.add_argument("--visited", type=int, default=-2,
@@ -304,28 +305,24 @@ def main():
     rows = torch.zeros((N + 1, dp), dtype=torch.float32, device=dev)
     rows[1:, :D] = torch.from_numpy(base).to(dev)
     qraw = torch.from_numpy(qry).to(dev)
-    ix = DeviceIndex(metric, "float", D, device=local)
-    ix.set_objects_device(rows.data_ptr(), N + 1)
     build_s = None
     tree = None
+    anng_check = None
     if args.graph == "anng":
-        # the index a user of `ngt create -g a -E <e>` gets, built by this
-        # library's own device construction (byte-identical to the
-        # reference's at C1, tests/test_gpu_build.py)
-        t0 = time.time()
-        (h_off, h_ids, _), tree = ix.build_anng(edge_size_for_creation=args.anng_edges, edge_size_for_search=es_prop)
-        build_s = time.time() - t0
-        offsets = torch.from_numpy(h_off.astype(np.int64)).to(dev)
-        edges = torch.from_numpy(h_ids.astype(np.int32)).to(dev)
-        log("ANNG (E=%d) built on the device in %.1f s: %d edges, mean degree %.1f" % (
-            args.anng_edges, build_s, edges.numel(), edges.numel() / N))
+        # the index a user of `ngt create -d 128 -o f -D 2 -E <e>` gets, built
+        # through the drop-in C API (ngt_create_graph_and_tree,
+        # ngt_batch_append_index, ngt_create_index -> this library's device
+        # construction, ngt_save_index), checked against the reference's own
+        # build of the same data (tests/golden/c2_anng_ref.json), and searched
+        # on the device index that handle serves (ngt_get_device_index)
+        ix, offsets, edges, tree, build_s, anng_check, cx = build_anng_capi(args, torch, dev, base, N, D, es_prop)
     else:
+        ix = DeviceIndex(metric, "float", D, device=local)
+        ix.set_objects_device(rows.data_ptr(), N + 1)
         offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev,
                                      cosine=c3)
-    ix.set_search_property(es_prop, 30, 20, args.seed_size, 0)
-    ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
-    if tree is not None:
-        ix.set_tree(tree)
+        ix.set_search_property(es_prop, 30, 20, args.seed_size, 0)
+        ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
     es_resolved = int(ix.resolve_edge_size(args.edge_size, 0.1))
     stream = torch.cuda.current_stream(dev).cuda_stream
     # queries prepared on the device like Index::allocateObject (pad; normalize
@@ -527,12 +524,45 @@ def main():
     traffic, tentry = measured_traffic(args.mode, args.config, graph, chosen, args.visited, filtered)
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
         tot = c[:, [5, 6, 1, 7, 3]].mean(0)
-        log("phase cycles/query: pop %.3g adjacency+visited %.3g filter %.3g eval %.3g accept+rest %.3g "
-            "(sum %.3g)" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum()))
+        if ix.last_search_lookahead() >= 0:
+            log("lookahead phase cycles/query: pop+targets %.3g adjacency %.3g filter %.3g exact %.3g commit %.3g "
+                "(sum %.3g); steps/query %.0f" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum(), c[:, 4].mean()))
+        else:
+            log("phase cycles/query: pop %.3g adjacency+visited %.3g filter %.3g eval %.3g accept+rest %.3g "
+                "(sum %.3g)" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum()))
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "qg":
         tot = c[:, [4, 5, 6, 7]].mean(0)
         log("phase cycles/query: pop %.3g ids %.3g codes+adc %.3g accept %.3g (sum %.3g)" % (
             tot[0], tot[1], tot[2], tot[3], tot.sum()))
+
+    # single-query launches (the reference's callers issue one query at a
+    # time, Capi.cpp:377-406): device time of nq=1 searches, sequentially
+    latency = None
+    if rank == 0 and not shard and not qgm and args.latency_queries > 0:
+        lat = []
+        lc = torch.zeros((args.latency_queries, COUNTERS), dtype=torch.int64, device=dev)
+        for i in range(args.latency_queries):
+            oi, od, on, _ = bufs[0]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ix.search_device(qdev[i:i + 1].data_ptr(), dp * 4, 1, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                             lc[i:i + 1].data_ptr(), k=K, epsilon=chosen, edge_size=args.edge_size,
+                             seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff[i:i + 2].data_ptr(),
+                             stream=stream, visited_hash_log2=0)
+            e1.record()
+            torch.cuda.synchronize()
+            lat.append(e0.elapsed_time(e1))
+        lat = np.array(lat)
+        latency = {"queries": len(lat), "mean_ms": float(lat.mean()), "p50_ms": float(np.percentile(lat, 50)),
+                   "p99_ms": float(np.percentile(lat, 99)), "form": ix.last_search_lookahead(),
+                   "what": "one query per launch (nq=1), full visited set, device time incl. launch"}
+        log("single-query launches: mean %.3f ms p50 %.3f p99 %.3f (lookahead form %d)" % (
+            latency["mean_ms"], latency["p50_ms"], latency["p99_ms"], latency["form"]))
+        if "stamps" in os.environ.get("NGT_AMD_LIB", ""):
+            lcc = lc.cpu().numpy().astype(np.float64)
+            tot = lcc[:, [5, 6, 1, 7, 3]].mean(0)
+            log("single-query phase cycles: pop+targets %.3g adjacency %.3g filter %.3g exact %.3g commit %.3g "
+                "(sum %.3g); steps %.0f" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum(), lcc[:, 4].mean()))
 
     cpu = parity = None
     if rank == 0 and not args.no_cpu and world == 1 and not shard:
@@ -546,6 +576,11 @@ def main():
                                    es_resolved=int(ix.resolve_edge_size(args.edge_size, chosen)))
         if scan is not None:
             scan["oracle_sample"] = scan_sample_check(rows, qdev, metric, K, gt_i, gt_d, gt_n)
+        if cpu is not None:
+            cpu["calibration"] = calibration()
+    ref_check = None
+    if rank == 0 and anng_check is not None and anng_check.get("reference"):
+        ref_check = reference_fixture_check(ix, qdev, dp, K, dev, torch)
 
     if rank == 0:
         if args.mode == "exact" and not c3:
@@ -614,6 +649,12 @@ def main():
             line["exact_scan"] = scan
         if build_s is not None:
             line["config"]["graph_build_s"] = build_s
+        if anng_check is not None:
+            line["config"]["construction_check"] = anng_check
+        if ref_check is not None:
+            line["config"]["reference_search_check"] = ref_check
+        if latency is not None:
+            line["single_query_latency"] = latency
         cn = tentry.get("counters_per_launch")
         if cn:
             # PMC evidence for what bounds the kernel (profiles/traffic.json):
@@ -656,6 +697,105 @@ def measured_traffic(mode, config, graph, eps, visited, filtered=False):
                 and bool(e.get("filtered", False)) == bool(filtered)):
             return float(e["traffic_bytes"]), e
     return None, {}
+
+
+def calibration():
+    """The oracle port against the reference itself, measured in the build
+    container on the same 1M ANNG, queries and epsilon
+    (tests/golden/make_c2_anng_fixture.py -> c2_anng_ref.json): the port's
+    single-thread QPS over the reference's.  On the GPU box only the port can
+    run; value / ratio is its reference-equivalent rate."""
+    path = os.path.join(ROOT, "tests", "golden", "c2_anng_ref.json")
+    if not os.path.exists(path):
+        return None
+    t = json.load(open(path))["timing"]
+    return {"where": "build container (%d CPUs), 1M x 128 ANNG built by the reference, %d queries, eps %g" % (
+                t["container_cores"], t["queries"], t["epsilon"]),
+            "reference_qps_1thread": t["reference_qps_1thread"], "port_qps_1thread": t["port_qps_1thread"],
+            "ratio_port_over_reference_1thread": t["ratio_port_over_reference_1thread"],
+            "port_identical_to_reference": t["port_identical_to_reference"]}
+
+
+def sha256_file(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 24), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def build_anng_capi(args, torch, dev, data, N, D, es_prop):
+    """ANNG + DVP tree through the C API, saved in the reference's format; the
+    saved files' sha256 against the reference build of the same data."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import ngt_files as F
+    from ngt_amd import base as capi
+    tmp = tempfile.mkdtemp(prefix="ngt_anng_")
+    capi.Index.create(tmp, D, edge_size_for_creation=args.anng_edges, edge_size_for_search=es_prop)
+    cx = capi.Index(tmp)
+    t0 = time.time()
+    cx.batch_append(data)
+    cx.build_index()
+    build_s = time.time() - t0
+    cx.save()
+    log("ANNG (E=%d) built through the C API in %.1f s (ngt_create_index on the device)" % (args.anng_edges, build_s))
+    check = {"reference": None}
+    ref_path = os.path.join(ROOT, "tests", "golden", "c2_anng_ref.json")
+    if os.path.exists(ref_path) and N == 1_000_000 and D == 128 and args.anng_edges == 10 and es_prop == 40:
+        ref = json.load(open(ref_path))
+        got = {f: sha256_file(os.path.join(tmp, f)) for f in ("obj", "grp", "tre")}
+        same = {f: got[f] == ref["build"]["sha256"][f] for f in got}
+        check = {"reference": "ngt create -d 128 -o f -D 2 -E 10 on the same data (%.0f s on %d CPUs)" % (
+                     ref["build"]["build_s"], ref["build"]["cpus"]),
+                 "files_identical": same}
+        log("construction vs the reference's files: %s" % same)
+    offs, ids, _ = F.read_grp(os.path.join(tmp, "grp"))
+    tree = F.read_tre(os.path.join(tmp, "tre"), D, np.float32)
+    offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    edges = torch.from_numpy(ids.astype(np.int32)).to(dev)
+    log("ANNG: %d edges, mean degree %.1f" % (edges.numel(), edges.numel() / N))
+    ix = cx.device_index()
+    shutil.rmtree(tmp, ignore_errors=True)
+    return ix, offsets, edges, tree, build_s, check, cx
+
+
+def reference_fixture_check(ix, qdev, dp, K, dev, torch):
+    """The device search of the reference fixture's queries at its epsilon
+    (tree seeds, the prf's edge size) against `ngt search`'s own output on its
+    own build of the same data (tests/golden/c2_anng_ref.npz): identical ids,
+    distances within the printed precision."""
+    from ngt_amd.device import SEED_TREE
+    path = os.path.join(ROOT, "tests", "golden", "c2_anng_ref.npz")
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "c2_anng_ref.json")))
+    z = np.load(path)
+    n = z["ids"].shape[0]
+    eps = float(meta["sweep"]["epsilon"])
+    oi = torch.zeros((n, K), dtype=torch.int32, device=dev)
+    od = torch.zeros((n, K), dtype=torch.float32, device=dev)
+    on = torch.zeros((n,), dtype=torch.int32, device=dev)
+    ix.search_device(qdev.data_ptr(), dp * 4, n, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None, k=K,
+                     epsilon=eps, edge_size=-1, seed_mode=SEED_TREE, stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    gi, gd, gn = oi.cpu().numpy().view(np.uint32), od.cpu().numpy(), on.cpu().numpy()
+    ids_same = bool(np.array_equal(gn, z["n"].astype(gn.dtype)))
+    dist_ok = True
+    for q in range(n if ids_same else 0):
+        m = int(gn[q])
+        ids_same = ids_same and np.array_equal(gi[q, :m], z["ids"][q, :m])
+        dist_ok = dist_ok and np.allclose(gd[q, :m], z["dists"][q, :m], rtol=1e-5, atol=0)
+    rec = recall_at(gi.astype(np.int64), z["truth"].astype(np.int64), K)
+    t = meta["timing"]
+    out = {"queries": n, "epsilon": eps, "ids_identical": ids_same, "distances_within_print_precision": dist_ok,
+           "recall_at_10_vs_reference_truth": rec,
+           "reference_qps_1thread_container": t["reference_qps_1thread"],
+           "reference_ms_per_query_1thread_container": t["reference_ms_per_query_1thread"]}
+    log("reference fixture (%d queries, eps %g): ids identical %s, distances %s" % (n, eps, ids_same, dist_ok))
+    if not (ids_same and dist_ok):
+        raise SystemExit("bench: the device search differs from the reference's own ngt search output")
+    return out
 
 
 def tree_seed_lists(ix, qdev, dp, nq, k, dev, torch):
@@ -933,7 +1073,9 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
     log("parity sample: %d queries identical to the oracle (ids, distance bits, work counters)" % done)
     what = ("NGTQG::Index::searchQuantizedGraph restatement (LUT as input)" if qg is not None
             else "searchReadOnlyGraph restatement")
+    cal = calibration()
     base = {"value": done / el, "unit": "queries/s", "cores": threads, "kind": "port",
+            "reference_equivalent_value": (done / el / cal["ratio_port_over_reference_1thread"]) if cal else None,
             "sample": "first %d of the %d queries (same graph, seeds, epsilon), oracle/ngt_oracle.c %s built -O3 "
                       "-march=x86-64-%s (16-lane FMA order kept), one query per thread on %d threads, %.1f s; "
                       "host: %s, %d CPUs" % (done, nq, what, isa, threads, el, model, ncpu)}

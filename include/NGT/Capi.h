@@ -21,7 +21,7 @@
  * undefined.
  *
  * Extensions (not in the reference): ngt_batch_search_index*,
- * ngt_get_last_search_counters, ngt_get_coalesce_stats.
+ * ngt_get_last_search_counters, ngt_get_coalesce_stats, ngt_get_device_index.
  */
 #ifndef NGT_AMD_CAPI_H
 #define NGT_AMD_CAPI_H
@@ -180,6 +180,11 @@ bool ngt_get_last_search_counters(NGTIndex, uint64_t *counters3, NGTError);
 /* single-query calls served so far: device launches issued and queries served
  * by them (served / batches = mean coalesced batch size) */
 bool ngt_get_coalesce_stats(NGTIndex, uint64_t *batches, uint64_t *served, NGTError);
+/* the device-resident index (an ngt_amd_index *, include/ngt_amd.h) serving
+ * this handle, built or refreshed from the host mirror on the call: for
+ * batched device-pointer searches on an index opened or built through this
+ * API.  Owned by the handle; valid until the next write to it or its close. */
+void *ngt_get_device_index(NGTIndex, NGTError);
 
 #ifdef __cplusplus
 }

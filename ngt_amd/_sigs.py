@@ -185,6 +185,7 @@ def declare(L):
                                                                u32p, f32p, u32p, vp]),
         "ngt_get_last_search_counters": (c_bool, [vp, u64p, vp]),
         "ngt_get_coalesce_stats": (c_bool, [vp, u64p, u64p, vp]),
+        "ngt_get_device_index": (vp, [vp, vp]),
         "ngt_set_property_value": (c_bool, [vp, c_char_p, c_char_p, vp]),
         "ngt_get_property_value": (c_int32, [vp, c_char_p, c_char_p, c_size_t, vp]),
         # ---- include/NGT/NGTQ/Capi.h

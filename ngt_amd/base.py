@@ -220,6 +220,22 @@ class Index(object):
             L.ngt_destroy_results(results)
             L.ngt_destroy_error_object(err)
 
+    def batch_append(self, objects):
+        """Append objects without building (ngt_batch_append_index); ids continue
+        from the repository size."""
+        o = np.ascontiguousarray(objects, dtype=np.float32)
+        self._check(self._L.ngt_batch_append_index(self.index, o.ctypes.data_as(POINTER(c_float)), o.shape[0],
+                                                   self.err), self.err)
+
+    def device_index(self):
+        """The DeviceIndex view of the ngt_amd_index this handle searches on
+        (ngt_get_device_index); valid until the next write or close."""
+        from .device import DeviceIndex
+        h = self._L.ngt_get_device_index(self.index, self.err)
+        if not h:
+            raise NativeError(_err_string(self._L, self.err))
+        return DeviceIndex.wrap(h, int(self.distance_type), "float" if self.is_float else "uint8", self.dim)
+
     def save(self, path=None):
         if path is None:
             path = self.path

@@ -1098,4 +1098,19 @@ bool ngt_get_coalesce_stats(NGTIndex index, uint64_t* batches, uint64_t* served,
   return true;
 }
 
+void* ngt_get_device_index(NGTIndex index, NGTError error) {
+  if (index == NULL) {
+    param_error(error, __FUNCTION__, "null index");
+    return NULL;
+  }
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  std::shared_lock<std::shared_mutex> rd;
+  std::string e = sync_device(ix, rd);
+  if (!e.empty()) {
+    set_error(error, __FUNCTION__, e);
+    return NULL;
+  }
+  return ix->dev;
+}
+
 }  // extern "C"

@@ -171,6 +171,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     // wave 0's sequential state
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, ndisc = 0, ns = 0;
+    // diagnostic build only: shader-clock totals per phase (wave 0's view)
+    uint64_t t_a = 0, t_b = 0, t_c = 0, t_e = 0, t_f = 0, t_last = 0, nsteps = 0;
+    (void)t_a; (void)t_b; (void)t_c; (void)t_e; (void)t_f; (void)t_last; (void)nsteps;
     float radius = a.radius;
     float expr = 0.f;
     double frq = 0.0;
@@ -445,6 +448,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     }
 
     // ---- best-first loop (Graph.cpp:430-486), P expansions per step --------
+#ifdef NGT_AMD_STAMPS
+    t_last = stamp();
+#endif
     for (;;) {
       // A. wave 0: pop the reference's next node, pick the next keys in line
       if (wave == 0) {
@@ -480,6 +486,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         }
       }
       __syncthreads();
+      NGT_MARK(t_a);
+      nsteps++;
       if (ctl->done) break;
       const uint32_t nt = ctl->nt;
 
@@ -534,6 +542,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if ((uint32_t)lane + 192 < c) L[o + 192 + lane] = r[jj][3];
       }
       __syncthreads();
+      NGT_MARK(t_b);
       const uint32_t nl = tot;
 
       // C. visited-at-step-start test + filter codes of every list entry:
@@ -634,6 +643,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       }
       __syncthreads();
 
+      NGT_MARK(t_c);
       // E. exact comparator distances of the survivors (bit-identical to
       // PrimitiveComparator::compareL2 through l2_fold_rows)
       {
@@ -660,6 +670,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         }
       }
       __syncthreads();
+      NGT_MARK(t_e);
 
       // F. wave 0 commits in the reference's pop order
       if (wave == 0) {
@@ -720,6 +731,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if (lane == 0 && done) ctl->done = 1;
       }
       __syncthreads();
+      NGT_MARK(t_f);
       if (ctl->done) break;
     }
 
@@ -741,6 +753,16 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           c[5] = maxq;
           c[6] = nexact;  // exact neighbour distances of the committed expansions
           c[7] = ns;
+#ifdef NGT_AMD_STAMPS
+          // phase cycles: [5] pop + targets, [6] adjacency + lists, [1] filter
+          // + survivors, [7] exact rows, [3] commit; [4] steps
+          c[5] = t_a;
+          c[6] = t_b;
+          c[1] = t_c;
+          c[7] = t_e;
+          c[3] = t_f;
+          c[4] = nsteps;
+#endif
         }
       }
     }

@@ -49,6 +49,22 @@ class DeviceIndex(object):
         self.h = h
         self.nrows = 0
 
+    @classmethod
+    def wrap(cls, handle, distance="l2", object_type="float", dim=128, nrows=0):
+        """A non-owning view of an existing ngt_amd_index (e.g. the one a C-API
+        handle serves its searches from, ngt_get_device_index)."""
+        self = cls.__new__(cls)
+        self.L = lib()
+        self.metric = DISTANCE[distance] if isinstance(distance, str) else int(distance)
+        self.otype = 2 if object_type in ("float", "f", 2) else 1
+        self.dtype = np.float32 if self.otype == 2 else np.uint8
+        self.dim = dim
+        self.dp = padded_dim(dim)
+        self.h = c_void_p(handle)
+        self.nrows = nrows
+        self._borrowed = True
+        return self
+
     # ---- data -------------------------------------------------------------
     def set_objects(self, rows, valid=None):
         """rows: [nrows, dim or padded dim] with row 0 the dummy slot."""
@@ -325,7 +341,8 @@ class DeviceIndex(object):
 
     def close(self):
         if getattr(self, "h", None):
-            self.L.ngt_amd_index_destroy(self.h)
+            if not getattr(self, "_borrowed", False):
+                self.L.ngt_amd_index_destroy(self.h)
             self.h = None
 
     def __del__(self):

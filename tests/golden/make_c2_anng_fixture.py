@@ -187,13 +187,16 @@ def stage_time(args, eps, gt):
         pp = os.path.join(args.work, "q_part%d.tsv" % p)
         write_tsv(pp, qs[sel])
         paths.append(pp)
-    t0 = time.time()
+    # each process's busy time = the sum of its per-query Timer values (the
+    # index load, seconds per process, is not search time)
+    outs = [open(pp + ".out", "w") for pp in paths]
     procs = [subprocess.Popen([args.ngt, "search", "-n", "10", "-e", str(eps), "-o", "e", idx, pp], env=env,
-                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for pp in paths]
-    for pr in procs:
+                              stdout=o, stderr=subprocess.DEVNULL) for pp, o in zip(paths, outs)]
+    for pr, o in zip(procs, outs):
         pr.wait()
-    wall = time.time() - t0
-    ref_qps_p = len(qs) / wall
+        o.close()
+    busy = [sum(x["time_ms"] for x in parse(open(pp + ".out").read())) / 1e3 for pp in paths]
+    ref_qps_p = len(qs) / max(busy)
     # the oracle restatement on the reference's own index files
     prf = ngt_files.read_prf(os.path.join(idx, "prf"))
     rows = ngt_files.read_obj(os.path.join(idx, "obj"), D, np.float32)[0]

@@ -51,7 +51,10 @@ def test_lookahead_matches_oracle(monkeypatch, nq, deg, visited):
     qs = rng.random((nq, dim), dtype=np.float32)
     seeds = [rng.choice(np.arange(1, n), 10, replace=False).astype(np.uint32) for _ in range(nq)]
     radius = float(np.sqrt(dim / 6.0))
+    # force the form under test (the default routing sends long lists of
+    # large launches to the one-expansion kernel)
     want_mode = 1 if nq < 2 * 256 else 0
+    monkeypatch.setenv("NGT_AMD_LA", "2" if want_mode == 1 else "1")
     for eps, rad, cq, es in [(0.0, -1.0, "", 0), (0.2, -1.0, "", 0), (1.0, -1.0, "64", 0), (-0.05, -1.0, "", 0),
                              (0.2, radius, "", 0), (0.3, -1.0, "", 40)]:
         if cq:
@@ -61,8 +64,7 @@ def test_lookahead_matches_oracle(monkeypatch, nq, deg, visited):
         gi, gd, gn, cnt = ix.search(qs, k=20, epsilon=eps, radius=rad, edge_size=es, seed_mode=SEED_GIVEN,
                                     seeds=seeds, visited_hash_log2=visited)
         mode = ix.last_search_lookahead()
-        if ix.L.ngt_amd_device_count() and os.environ.get("NGT_AMD_LA", "3") == "3":
-            assert mode == want_mode, (mode, want_mode)
+        assert mode == want_mode, (mode, want_mode)
         kw = {} if rad < 0 else {"radius": rad}
         oi, od, on, oc = O.search_batch("l2", rows, offs, edges, qs, seeds, 20, np.float32(eps), edge_size=es,
                                         threads=os.cpu_count() or 1, **kw)
@@ -108,7 +110,7 @@ def test_lookahead_equals_single_expansion_kernel(monkeypatch, name):
     ix = device_index(name)[0]
     qs = np.tile(queries(), (6, 1))  # 600 queries: the wave-per-query form
     out = {}
-    for la in ["0", "3"]:
+    for la in ["0", "1", "2"]:  # off, the wave-per-query form forced, the 8-wave form
         monkeypatch.setenv("NGT_AMD_LA", la)
         for nq in (40, 600):
             for eps in (0.0, 0.1):
@@ -116,7 +118,8 @@ def test_lookahead_equals_single_expansion_kernel(monkeypatch, name):
                 out[(la, nq, eps)] = (gi, gd, gn, cnt, ix.last_search_lookahead())
     for nq in (40, 600):
         for eps in (0.0, 0.1):
-            a, b = out[("0", nq, eps)], out[("3", nq, eps)]
+            la = "2" if nq < 512 else "1"
+            a, b = out[("0", nq, eps)], out[(la, nq, eps)]
             assert a[4] == -1 and b[4] == (1 if nq < 512 else 0)
             assert np.array_equal(a[2], b[2])
             assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
