@@ -580,9 +580,21 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       const char* v = getenv("NGT_AMD_LA_LMAX");
       return v ? (uint32_t)std::max(256, std::min(8192, atoi(v))) : 0u;
     }();
-    a.la_lmax = env_lmax ? env_lmax : (la_mode == 0 ? 256u : 2048u);
+    // list capacity: the targets' lists of the longest kind (t0's always fits)
+    const uint32_t deg_cap = (uint32_t)std::min<uint64_t>(a.adj_stride, a.edge_size);
+    const uint32_t P = la_targets(la_mode);
+    a.la_lmax = env_lmax ? env_lmax
+                         : (la_mode == 0 ? std::max<uint32_t>(deg_cap, std::min<uint32_t>(256u, (P * deg_cap + 15) & ~15u))
+                                         : 2048u);
+    a.la_lmax = std::max<uint32_t>(a.la_lmax, deg_cap);
+    // per-step id set: twice the ids a step can insert -- every list entry
+    // with the full visited set; the accepted-only set inserts only accepted
+    // ids, and the commit loop stops before a target could overfill it, so
+    // there 4 x the longest list is plenty (and keeps 12+ waves per CU)
+    const uint32_t sh_want = (la_mode == 0 && a.accepted_only) ? std::min<uint32_t>(2u * a.la_lmax, 4u * deg_cap)
+                                                               : 2u * a.la_lmax;
     a.la_sh_log2 = 1;
-    while ((1u << a.la_sh_log2) < 2u * a.la_lmax) a.la_sh_log2++;
+    while ((1u << a.la_sh_log2) < sh_want) a.la_sh_log2++;
     if (a.vf_log2 == 0) a.vf_log2 = 15;
     a.cq_cap = la_mode == 0 ? 512u : 2048u;
     if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));

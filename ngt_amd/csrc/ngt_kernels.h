@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace ngt_amd {
 
@@ -95,7 +96,11 @@ struct SearchArgs {
 
 // lookahead targets per step of search_la.hip: mode 0 (throughput, one wave
 // per query), mode 1 (latency, eight waves per query)
-inline uint32_t la_targets(int mode) { return mode == 0 ? 4u : 8u; }
+inline uint32_t la_targets(int mode) {
+  if (mode != 0) return 8u;
+  const char* v = getenv("NGT_AMD_LA_P");  // 3 or 4 (default)
+  return v && atoi(v) == 3 ? 3u : 4u;
+}
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint32_t slots, hipStream_t s);
 

@@ -171,6 +171,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     // wave 0's sequential state
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, ndisc = 0, ns = 0;
+    uint32_t sh_used = 0;  // ids inserted into this step's id set
     // diagnostic build only: shader-clock totals per phase (wave 0's view)
     uint64_t t_a = 0, t_b = 0, t_c = 0, t_e = 0, t_f = 0, t_last = 0, nsteps = 0;
     (void)t_a; (void)t_b; (void)t_c; (void)t_e; (void)t_f; (void)t_last; (void)nsteps;
@@ -385,13 +386,62 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
     // order (Graph.cpp:471-483); only candidates within the radius at batch
     // start can be accepted
+    // Push the candidates of `bm` (lanes of nid/nd, all within the
+    // exploration radius and none within the result radius, so none changes
+    // either radius) into the unchecked set at once -- what the sequential
+    // accept would do for each of them.
+    auto push_batch = [&](uint64_t bm) {
+      const uint32_t cnt = (uint32_t)__popcll(bm);
+      if (cnt == 0) return;
+      const bool mine = (bm >> lane) & 1ull;
+      const uint32_t id = mine ? nid[lane] : 0u;
+      const uint64_t key = mine ? make_key(nd[lane], id) : ~0ull;
+      if constexpr (!FULL) {
+        if (mine) {
+          vf_set(vf, vf_shift, id);
+          vis[id] = (uint8_t)epoch;
+          sh_insert(sh, a.la_sh_log2, id);
+        }
+        sh_used += cnt;
+      }
+      const bool below = ballot64(mine && key >= T) == 0ull;
+      if (below && ncq + cnt <= a.cq_cap) {
+        const uint32_t n0 = ncq;
+        if (mine) cq[n0 + mbcnt(bm)] = key;
+        ncq += cnt;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t c = n0 >> 6; c <= (ncq - 1) >> 6; c++) chunk_min(c);
+        __builtin_amdgcn_wave_barrier();
+        if (ncq + nspill > maxq) maxq = ncq + nspill;
+      } else {
+        uint64_t r = bm;
+        while (r) {
+          const int j = __ffsll((long long)r) - 1;
+          r &= r - 1;
+          insert_key(__shfl(key, j, 64));
+        }
+      }
+    };
+    // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
+    // order (Graph.cpp:471-483).  Only a candidate within the RESULT radius
+    // changes the state the next candidates see (it enters the results and
+    // may shrink both radii), so the candidates before the next such one are
+    // pushed as one batch, that one alone, and the rest re-tested against the
+    // new exploration radius -- the sequential order's outcome exactly.
     auto accept = [&](uint32_t me) {
-      uint64_t okmask = ballot64((uint32_t)lane < me && nd[lane] <= expr);
+      const float dl = (uint32_t)lane < me ? nd[lane] : 0.f;
+      const bool inl = (uint32_t)lane < me;
+      uint64_t okmask = ballot64(inl && dl <= expr);
       while (okmask) {
-        const int j = __ffsll((long long)okmask) - 1;
-        okmask &= okmask - 1;
+        const uint64_t rmask = okmask & ballot64(inl && dl <= radius);
+        if (rmask == 0ull) {
+          push_batch(okmask);
+          break;
+        }
+        const int j = __ffsll((long long)rmask) - 1;
+        push_batch(okmask & ((1ull << j) - 1ull));
+        // candidate j: d <= radius <= explorationRadius
         const float d = nd[j];
-        if (!(d <= expr)) continue;
         const uint32_t id = nid[j];
         const uint64_t key = make_key(d, id);
         if constexpr (!FULL) {
@@ -400,16 +450,17 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             vis[id] = (uint8_t)epoch;
             sh_insert(sh, a.la_sh_log2, id);
           }
+          sh_used++;
         }
         insert_key(key);
-        if (d <= radius) {
-          res_insert(res, nres, k, key);
-          if (nres >= k) {
-            radius = key_dist(res[k - 1]);
-            expr = __fmul_rn(a.coef, radius);
-          }
+        res_insert(res, nres, k, key);
+        if (nres >= k) {
+          radius = key_dist(res[k - 1]);
+          expr = __fmul_rn(a.coef, radius);
         }
         __builtin_amdgcn_wave_barrier();
+        okmask &= ~((2ull << j) - 1ull);  // the candidates after j ...
+        okmask &= ballot64(inl && dl <= expr);  // ... within the (possibly smaller) radius
       }
     };
 
@@ -465,18 +516,37 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         } else {
           if (lane == 0) tkey[0] = key;
           nt = 1;
-          uint64_t prev = key;
-          for (int j = 1; j < P; j++) {
-            uint64_t m = ~0ull;
+          if constexpr (P > 1) {
+            // the next P - 1 keys in line (all LDS keys are > key; spill keys
+            // are larger still): every lane keeps its two smallest keys, the
+            // wave takes the minimum of the lanes' heads P - 1 times, and a
+            // lane that runs out of heads rescans its share above the last
+            // key it gave
+            uint64_t h0 = ~0ull, h1 = ~0ull;
             for (uint32_t i = lane; i < ncq; i += 64) {
               const uint64_t v = cq[i];
-              if (v > prev && v < m) m = v;
+              if (v < h1) {
+                if (v < h0) { h1 = h0; h0 = v; } else { h1 = v; }
+              }
             }
-            m = wave_min_u64(m);
-            if (m == ~0ull || key_dist(m) > expr) break;
-            if (lane == 0) tkey[j] = m;
-            prev = m;
-            nt++;
+            for (int j = 1; j < P; j++) {
+              const uint64_t m = wave_min_u64(h0);
+              if (m == ~0ull || key_dist(m) > expr) break;
+              if (lane == 0) tkey[j] = m;
+              nt++;
+              if (h0 == m) {  // keys are distinct: one owner
+                h0 = h1;
+                h1 = ~0ull;
+                if (h0 == ~0ull) {
+                  for (uint32_t i = lane; i < ncq; i += 64) {
+                    const uint64_t v = cq[i];
+                    if (v > m && v < h1) {
+                      if (v < h0) { h1 = h0; h0 = v; } else { h1 = v; }
+                    }
+                  }
+                }
+              }
+            }
           }
         }
         if (lane == 0) {
@@ -675,8 +745,15 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       // F. wave 0 commits in the reference's pop order
       if (wave == 0) {
         uint32_t done = 0;
+        sh_used = 0;
         for (uint32_t j = 0; j < ntl_s; j++) {
           if (j > 0) {
+            // the step's id set must never fill: stop before a target whose
+            // every entry could be inserted would pass half its capacity
+            if (sh_used + (loff[j + 1] - loff[j]) > sh_n / 2) {
+              ndisc += ntl_s - j;
+              break;
+            }
             uint32_t bidx;
             const uint64_t m = find_min(bidx);
             if (m == ~0ull || key_dist(m) > expr) {  // the reference stops here (Graph.cpp:433-435)
@@ -707,14 +784,16 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             const uint32_t xi = xr + mbcnt(kmask);
             xr += (uint32_t)__popcll(kmask);
             const bool fresh = (fl & 1u) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
+            const uint32_t nfresh = (uint32_t)__popcll(ballot64(fresh));
             if constexpr (FULL) {
               if (fresh) {
                 vf_set(vf, vf_shift, id);
                 vis[id] = (uint8_t)epoch;
                 sh_insert(sh, a.la_sh_log2, id);
               }
+              sh_used += nfresh;
             }
-            ndist += (uint32_t)__popcll(ballot64(fresh));
+            ndist += nfresh;
             const bool keep = fresh && (fl & 2u);
             const uint64_t km = ballot64(keep);
             if (keep) {
@@ -788,16 +867,26 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
     hipLaunchKernelGGL(kern, dim3(slots), dim3(64 * W), lds, s, a);                                             \
   } while (0)
   if (mode == 0) {
-    if (a.dp == 128) {
-      if (full) LA(8, 1, 4, 6, 1, true); else LA(8, 1, 4, 6, 1, false);
+    if (P == 3) {
+      if (a.dp == 128) {
+        if (full) LA(8, 1, 3, 6, 1, true); else LA(8, 1, 3, 6, 1, false);
+      } else {
+        if (full) LA(6, 1, 3, 6, 1, true); else LA(6, 1, 3, 6, 1, false);
+      }
     } else {
-      if (full) LA(6, 1, 4, 6, 1, true); else LA(6, 1, 4, 6, 1, false);
+      if (a.dp == 128) {
+        if (full) LA(8, 1, 4, 6, 1, true); else LA(8, 1, 4, 6, 1, false);
+      } else {
+        if (full) LA(6, 1, 4, 6, 1, true); else LA(6, 1, 4, 6, 1, false);
+      }
     }
   } else {
+    // latency form: one workgroup per CU, 2 waves per SIMD -> room for 192
+    // filter rows in flight per wave (1,536 per step's round trip)
     if (a.dp == 128) {
-      if (full) LA(8, 8, 1, 4, 1, true); else LA(8, 8, 1, 4, 1, false);
+      if (full) LA(8, 8, 1, 12, 1, true); else LA(8, 8, 1, 12, 1, false);
     } else {
-      if (full) LA(6, 8, 1, 4, 1, true); else LA(6, 8, 1, 4, 1, false);
+      if (full) LA(6, 8, 1, 12, 1, true); else LA(6, 8, 1, 12, 1, false);
     }
   }
 #undef LA
