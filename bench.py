@@ -393,12 +393,15 @@ def main():
         # 1600-object sample as the reference's dynamic k-means), encoder,
         # quantized graph (QuantizedGraph.h:456-475)
         t0 = time.time()
-        _, its = ix.qg_train(D, nsample=1600, max_iter=20)
+        h_base = np.zeros((min(N, 1600) + 1, D), np.float32)
+        h_base[1:] = base[:min(N, 1600)]
+        qg_local = ix.qg_train_ngt(h_base, dsub=1)  # ngtqg_quantize's kmeansWithNGT codebooks
+        t1 = time.time()
         ix.qg_encode(return_codes=False)
         ix.qg_build_graph(None, args.qg_edges)
         torch.cuda.synchronize()
-        log("quantizer (k-means %d-%d iterations) + encoder + quantized graph in %.1f s (degree <= %d)" % (
-            its.min(), its.max(), time.time() - t0, ix.qg_max_degree()))
+        log("quantizer (kmeansWithNGT, %d subspaces) %.1f s + encoder + quantized graph %.1f s (degree <= %d)" % (
+            D, t1 - t0, time.time() - t1, ix.qg_max_degree()))
 
     def run(eps, si=0, visited=None, nq=NQ):
         oi, od, on, oc = bufs[si]
@@ -573,7 +576,8 @@ def main():
         torch.cuda.synchronize()
         gpu_out = (out_i.cpu().numpy().view(np.uint32), out_d.cpu().numpy(), out_n.cpu().numpy().view(np.uint32))
         cpu, parity = cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, chosen, metric, gpu_out, full_cnt,
-                                   es_resolved=int(ix.resolve_edge_size(args.edge_size, chosen)))
+                                   es_resolved=int(ix.resolve_edge_size(args.edge_size, chosen)),
+                                   qg_local=qg_local if qgm else None)
         if scan is not None:
             scan["oracle_sample"] = scan_sample_check(rows, qdev, metric, K, gt_i, gt_d, gt_n)
         if cpu is not None:
@@ -993,7 +997,18 @@ def scan_sample_check(rows, qdev, metric, k, gt_i, gt_d, gt_n, nsample=16):
     return {"queries": nsample, "identical": True}
 
 
-def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_out, gpu_cnt, es_resolved=0):
+def qg_luts_oracle(O, qgo, h_q, n):
+    luts, scs, tos = [], [], []
+    for i in range(n):
+        lut, sc, to = O.qg_lut(qgo, h_q[i])
+        luts.append(lut)
+        scs.append(sc)
+        tos.append(to)
+    return np.stack(luts), np.array(scs, np.float32), np.array(tos, np.float32)
+
+
+def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_out, gpu_cnt, es_resolved=0,
+                 qg_local=None):
     """The CPU baseline and the parity sample in one: the oracle restatement
     (oracle/ngt_oracle.c, the reference's 16-lane FMA order) built -O3 for the
     host's widest ISA (x86-64-v4 AVX-512, else v3) with one query per thread on
@@ -1021,7 +1036,11 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
         qg = {"M": args.dim, "qids": ids[ids != 0].astype(np.uint32),
               "qoff": qoff, "code_off": (np.arange(len(deg) + 1, dtype=np.uint64) * np.uint64(codes.shape[1])),
               "codes": np.ascontiguousarray(codes.reshape(-1))}
-        lut, sc, to = ix.qg_lut(h_q[:, :args.dim])
+        # the LUTs from the oracle's createDistanceLookup (Quantizer.h:709-760)
+        # on the same codebooks: the sample checks LUT + ADC + search
+        qgo = {"M": args.dim, "dim": args.dim, "dsub": 1, "global": np.zeros(args.dim, np.float32),
+               "local": qg_local}
+        lut, sc, to = qg_luts_oracle(O, qgo, h_q, min(h_q.shape[0], 20000))
     log("cpu baseline: host copy %.1f s; %s, %d CPUs, %d threads, oracle %s build" % (
         time.time() - t0, model, ncpu, threads, isa))
 
@@ -1071,7 +1090,8 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
     if not (same and cnt_same):
         raise SystemExit("bench: the device results differ from the oracle on the parity sample: %s" % parity)
     log("parity sample: %d queries identical to the oracle (ids, distance bits, work counters)" % done)
-    what = ("NGTQG::Index::searchQuantizedGraph restatement (LUT as input)" if qg is not None
+    what = ("NGTQG::Index::searchQuantizedGraph restatement (LUT, ADC, search and rerank from the raw "
+            "queries on the kmeansWithNGT codebooks)" if qg is not None
             else "searchReadOnlyGraph restatement")
     cal = calibration()
     base = {"value": done / el, "unit": "queries/s", "cores": threads, "kind": "port",

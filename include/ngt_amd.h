@@ -393,6 +393,12 @@ int ngt_amd_sharded_qg_search_device(ngt_amd_shard_comm *comm, ngt_amd_index *in
                                      uint32_t *d_out_ids, float *d_out_dists, uint32_t *d_out_n,
                                      void *stream);
 
+/* The local codebooks ngtqg_quantize trains: the kmeansWithNGT restatement
+ * (lib/NGT/Clustering.h:648-760, as NGTQ drives it, NGTQ/Quantizer.h:1802-1858)
+ * over the first 1,600 objects of rows [nrows][dim] (row 0 the dummy slot);
+ * local_out [dim/dsub][16][dsub]. */
+int ngt_amd_qg_train_local_ngt(const float *rows, uint64_t nrows, uint32_t dim, uint32_t dsub, float *local_out);
+
 /* ---- NGTQ IVF-ADC ------------------------------------------------------- *
  *   ngt_amd_ngtq_open          <- NGTQ::Index(path) (lib/NGT/NGTQ/Quantizer.h:2832-2836,
  *                                 QuantizerInstance::open :1520-1570): prf, global/

@@ -66,6 +66,7 @@ def declare(L):
         "ngt_amd_search": (c_int, [vp, POINTER(SearchParams), vp, c_uint32, vp, vp, vp, vp, vp, vp]),
         "ngt_amd_tree_seeds_device": (c_int, [vp, vp, c_uint64, c_uint32, c_uint32, vp, c_uint32, vp, vp]),
         "ngt_amd_last_search_lookahead": (c_int, [vp]),
+        "ngt_amd_qg_train_local_ngt": (c_int, [vp, c_uint64, c_uint32, c_uint32, vp]),
         "ngt_amd_search_device": (c_int, [vp, POINTER(SearchParams), vp, c_uint64, c_uint32, vp, vp, vp, vp,
                                           vp, vp, vp]),
         "ngt_amd_linear_search": (c_int, [vp, vp, c_uint32, c_uint32, c_double, vp, vp, vp]),

@@ -590,7 +590,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     // per-step id set: twice the ids a step can insert -- every list entry
     // with the full visited set; the accepted-only set inserts only accepted
     // ids, and the commit loop stops before a target could overfill it, so
-    // there 4 x the longest list is plenty (and keeps 12+ waves per CU)
+    // there 4 x the longest list is plenty (and keeps 12 waves per CU)
     const uint32_t sh_want = (la_mode == 0 && a.accepted_only) ? std::min<uint32_t>(2u * a.la_lmax, 4u * deg_cap)
                                                                : 2u * a.la_lmax;
     a.la_sh_log2 = 1;

@@ -98,8 +98,8 @@ struct SearchArgs {
 // per query), mode 1 (latency, eight waves per query)
 inline uint32_t la_targets(int mode) {
   if (mode != 0) return 8u;
-  const char* v = getenv("NGT_AMD_LA_P");  // 3 or 4 (default)
-  return v && atoi(v) == 3 ? 3u : 4u;
+  const char* v = getenv("NGT_AMD_LA_P");  // 3 (default: fewer discarded targets per step) or 4
+  return v && atoi(v) == 4 ? 4u : 3u;
 }
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint32_t slots, hipStream_t s);

@@ -22,6 +22,7 @@
 #include "../../include/NGT/NGTQ/Capi.h"
 #include "../../include/ngt_amd.h"
 #include "coalesce.h"
+#include "index_internal.h"
 #include "index_io.h"
 #include "kmeans_ngt.h"
 
@@ -301,6 +302,33 @@ static std::string train_local_kmeans_ngt(const ngt_amd::HostIndex& h, uint32_t 
     if (!e.empty()) return "local codebook " + std::to_string(m) + ": " + e;
   }
   return "";
+}
+
+// The local codebooks ngtqg_quantize trains (train_local_kmeans_ngt: the
+// kmeansWithNGT restatement over the first 1,600 objects, Quantizer.h:1802-1858,
+// Clustering.h:648-760), for callers that hold the objects themselves:
+// rows = [nrows][dim] floats, row 0 the dummy slot; local = [M][16][dsub].
+extern "C" int ngt_amd_qg_train_local_ngt(const float* rows, uint64_t nrows, uint32_t dim, uint32_t dsub,
+                                          float* local_out) {
+  if (!rows || !local_out || dim == 0 || dsub == 0 || dim % dsub != 0 || nrows < 17)
+    return ngt_amd::fail("ngt_amd_qg_train_local_ngt: bad arguments");
+  ngt_amd::HostIndex h;
+  h.prop.dimension = (int32_t)dim;
+  h.prop.object_type = NGT_AMD_OBJECT_FLOAT;
+  h.prop.distance_type = NGT_AMD_DISTANCE_L2;
+  h.init_layout();
+  const uint64_t n = std::min<uint64_t>(nrows, 1601);  // the sample is the first 1,600 objects
+  h.nrows = n;
+  h.rows.assign((size_t)n * h.row_bytes, 0);
+  h.valid.assign(n, 1);
+  h.valid[0] = 0;
+  for (uint64_t i = 1; i < n; i++) memcpy(h.rows.data() + i * h.row_bytes, rows + i * dim, (size_t)dim * 4);
+  std::vector<float> local;
+  const uint32_t M = dim / dsub;
+  std::string e = train_local_kmeans_ngt(h, M, dsub, local);
+  if (!e.empty()) return ngt_amd::fail("ngt_amd_qg_train_local_ngt: %s", e.c_str());
+  std::copy(local.begin(), local.end(), local_out);
+  return 0;
 }
 
 // NGTQG::Index::quantize (lib/NGT/NGTQ/QuantizedGraph.h:456-475) on the device:

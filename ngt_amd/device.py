@@ -270,6 +270,18 @@ class DeviceIndex(object):
         self.qg_Me = (M + 1) // 2 * 2
         return loc, its
 
+    def qg_train_ngt(self, rows, dsub=1):
+        """The codebooks ngtqg_quantize would train (kmeansWithNGT restatement,
+        ngt_amd_qg_train_local_ngt) from host rows [nrows][>= dim] (row 0 the
+        dummy slot), set as this index's quantizer (zero global centroid,
+        QuantizedGraph.h:397-399); returns local [M][16][dsub]."""
+        r = np.ascontiguousarray(np.asarray(rows, np.float32)[:1601, :self.dim])
+        M = self.dim // dsub
+        local = np.zeros((M, 16, dsub), np.float32)
+        _chk(self.L.ngt_amd_qg_train_local_ngt(r.ctypes.data, r.shape[0], self.dim, dsub, local.ctypes.data))
+        self.qg_set_quantizer(np.zeros(self.dim, np.float32), local)
+        return local
+
     def qg_set_graph(self, qoff, qids, code_off, codes):
         qoff = np.ascontiguousarray(qoff, dtype=np.uint64)
         qids = np.ascontiguousarray(qids if len(qids) else np.zeros(1), dtype=np.uint32)

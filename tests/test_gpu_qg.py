@@ -434,3 +434,16 @@ def test_ngtqg_quantize_codebooks_dsub4(tmp_path):
     for m in range(5):
         rows, _ = F.read_obj(os.path.join(str(d), "qg", "local-%d" % m, "obj"), 4, np.float32)
         assert np.array_equal(rows[1:17, :4].view(np.uint32), st[m].view(np.uint32)), m
+
+
+def test_qg_train_local_ngt_equals_reference_codebooks():
+    """DeviceIndex.qg_train_ngt (ngt_amd_qg_train_local_ngt, the codebook
+    training ngtqg_quantize runs, used by bench.py --mode qg) on the C1 objects:
+    the reference's single-thread `ngtqg quantize` codebooks bit for bit."""
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("c1_qg")
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows, valid)
+    local = ix.qg_train_ngt(rows, dsub=1)
+    st = np.load(os.path.join(GOLD, "qg_kmeans_st.npz"))["c1"]
+    assert np.array_equal(local[:, :, 0].view(np.uint32), st.view(np.uint32))
+    ix.close()
