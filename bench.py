@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--qg", action="store_true", help="with --mode shard: NGTQG shards (C5's form)")
     ap.add_argument("--config", choices=["c2", "c3"], default="c2")
     ap.add_argument("--n", type=int, default=0, help="objects (per shard in --mode shard)")
+    ap.add_argument("--shards-per-gpu", type=int, default=1, help="--mode shard: shards each rank holds")
+    ap.add_argument("--shard-sample", type=int, default=2000, help="--mode shard: oracle parity sample (queries)")
     ap.add_argument("--dim", type=int, default=0)
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
@@ -226,6 +228,8 @@ def main():
                     help="knn: exact kNN graph built in setup (out/in edges); anng: this library's own "
                          "ngt_create_index ANNG (GraphAndTreeIndex::createIndex on the device)")
     ap.add_argument("--anng-edges", type=int, default=10, help="--graph anng: edgeSizeForCreation (ngt create -E)")
+    ap.add_argument("--anng-dir", type=str, default="",
+                    help="--graph anng: keep the saved index here, or open it if an earlier run saved it")
     ap.add_argument("--edge-size", type=int, default=None,
                     help="sc.edgeSize of the searches (getEdgeSize, Graph.h:675-692): -1 = the index's "
                          "EdgeSizeForSearch (an `ngt create` index: 40), 0 = every edge; default -1 for "
@@ -245,6 +249,8 @@ def main():
     ap.add_argument("--sweep-nq", type=int, default=2000, help="queries per epsilon-sweep launch")
     ap.add_argument("--latency-queries", type=int, default=100, help="single-query launches timed after the bench")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-launches", type=int, default=0,
+                    help="after the epsilon is set: run this many launches of the timed configuration and exit")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
     ap.add_argument("--visited", type=int, default=-2,
                     help="visited set: -2 HBM epochs of accepted ids, -1 HBM epochs of every evaluated id "
@@ -285,6 +291,8 @@ def main():
     from ngt_amd.device import COUNTERS, SEED_GIVEN, DeviceIndex
     if args.mode == "capi":
         return capi_bench(args, torch, dev, result_out)
+    if args.mode == "shard":
+        return shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm)
 
     N, D, NQ, K = args.n, args.dim, args.nq, args.k
     dp = ((D - 1) // 16 + 1) * 16
@@ -451,6 +459,16 @@ def main():
         chosen = float(t.item())
         rec = measure(chosen, NQ)
 
+    if args.pmc_launches:
+        # counter passes (scripts/pmc_r3.sh): exactly this many more launches of
+        # the timed configuration, nothing else of the bench
+        for _ in range(args.pmc_launches):
+            run(chosen)
+            torch.cuda.synchronize()
+        print(json.dumps({"pmc_launches": args.pmc_launches, "epsilon": chosen, "recall_at_10": rec,
+                          "launches_before": len(sweep), "kernel_ms_last": ix.last_search_kernel_ms()}),
+              file=result_out, flush=True)
+        return
     for i in range(max(args.warmup, nstreams)):
         run(chosen, i % nstreams)
     torch.cuda.synchronize()
@@ -503,6 +521,10 @@ def main():
     ne = c[:, 2]
     log("expansions/query: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %.0f" % (
         ne.mean(), np.percentile(ne, 50), np.percentile(ne, 90), np.percentile(ne, 99), ne.max()))
+    la_form = -1 if qgm else ix.last_search_lookahead()
+    if la_form >= 0 and "stamps" not in os.environ.get("NGT_AMD_LIB", ""):
+        log("lookahead form %d: %.0f speculative expansions discarded/query (%.0f committed)" % (
+            la_form, c[:, 3].mean(), ne.mean()))
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     graph = ("kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg) if args.graph == "knn"
              else "ANNG E%d (ngt_create_index on the device)" % args.anng_edges)
@@ -667,6 +689,15 @@ def main():
                 "source": tentry.get("source", ""), "SQ_INSTS_VALU": cn["SQ_INSTS_VALU"],
                 "valu_wave_cycle_frac": cn["SQ_ACTIVE_INST_VALU"] / cn["SQ_WAVE_CYCLES"],
                 "traffic_over_algorithmic": traffic / alg_bytes}
+            if "SQ_WAIT_ANY" in cn:
+                # the wave-cycle partition (MI355X_MICROARCH.md rocprofv3 PMC slots):
+                # parked on s_waitcnt/barrier, issue-stalled, issuing
+                w = cn["SQ_WAVE_CYCLES"]
+                line["roofline"]["counters"].update({
+                    "wait_any_frac": cn["SQ_WAIT_ANY"] / w, "wait_inst_any_frac": cn["SQ_WAIT_INST_ANY"] / w,
+                    "active_inst_any_frac": cn["SQ_ACTIVE_INST_ANY"] / w,
+                    "SQ_INSTS_LDS": cn.get("SQ_INSTS_LDS"),
+                    "trace_avg_kernel_ms": tentry.get("trace_avg_kernel_ms")})
         if qgm:
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
@@ -695,7 +726,7 @@ def measured_traffic(mode, config, graph, eps, visited, filtered=False):
             entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
         return None, {}
-    for e in entries:
+    for e in reversed(entries):  # the newest entry for the workload
         if (e.get("mode", "exact") == mode and e.get("config", "c2") == config and e["graph"] == graph
                 and e.get("visited", -1) == visited and abs(e["epsilon"] - eps) < 1e-7
                 and bool(e.get("filtered", False)) == bool(filtered)):
@@ -737,7 +768,19 @@ def build_anng_capi(args, torch, dev, data, N, D, es_prop):
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import ngt_files as F
     from ngt_amd import base as capi
-    tmp = tempfile.mkdtemp(prefix="ngt_anng_")
+    keep = args.anng_dir
+    if keep and os.path.exists(os.path.join(keep, "grp")):
+        # a directory an earlier run of this bench built and saved: opened with
+        # ngt_open_index (the construction check belongs to the run that built it)
+        cx = capi.Index(keep)
+        offs, ids, _ = F.read_grp(os.path.join(keep, "grp"))
+        tree = F.read_tre(os.path.join(keep, "tre"), D, np.float32)
+        log("ANNG opened from %s (built by an earlier run)" % keep)
+        return (cx.device_index(), torch.from_numpy(offs.astype(np.int64)).to(dev),
+                torch.from_numpy(ids.astype(np.int32)).to(dev), tree, None, {"reference": None, "reopened": keep}, cx)
+    tmp = keep or tempfile.mkdtemp(prefix="ngt_anng_")
+    if keep:
+        os.makedirs(os.path.dirname(os.path.abspath(keep)), exist_ok=True)
     capi.Index.create(tmp, D, edge_size_for_creation=args.anng_edges, edge_size_for_search=es_prop)
     cx = capi.Index(tmp)
     t0 = time.time()
@@ -762,7 +805,8 @@ def build_anng_capi(args, torch, dev, data, N, D, es_prop):
     edges = torch.from_numpy(ids.astype(np.int32)).to(dev)
     log("ANNG: %d edges, mean degree %.1f" % (edges.numel(), edges.numel() / N))
     ix = cx.device_index()
-    shutil.rmtree(tmp, ignore_errors=True)
+    if not keep:
+        shutil.rmtree(tmp, ignore_errors=True)
     return ix, offsets, edges, tree, build_s, check, cx
 
 
@@ -953,6 +997,285 @@ def capi_bench(args, torch, dev, result_out):
     ix.close()
 
 
+def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
+    """C4's and C5's form: the object repository as
+    world x S shards of --n objects, rank r holding shards r*S .. r*S+S-1
+    (global ids offset by shard * n), every shard an independent index with
+    its own graph (and, with --qg, its own NGTQG quantizer, encoder and
+    quantized graph).  A step searches the whole batch on every shard -- the
+    S local shards concurrently on S streams -- packs the S top-k lists into
+    the rank's one RCCL all-gather message and merges world * S lists on the
+    device (ngt_amd/shard.py).  S > 1 serves an index larger than one graph a
+    run can build on one GPU (C4's 10M on one GPU: S = 8 shards of 1.25M)."""
+    from ngt_amd.device import COUNTERS, SEED_GIVEN, DeviceIndex
+    from ngt_amd.shard import ShardedIndex
+    N, D, NQ, K = args.n, args.dim, args.nq, args.k
+    S = max(1, args.shards_per_gpu)
+    dp = ((D - 1) // 16 + 1) * 16
+    t0 = time.time()
+    qry = splitmix_uniform(NQ, D, BASE_SEED + 1)
+    shards = []
+    for s in range(S):
+        off = (rank * S + s) * N
+        base = splitmix_uniform(N, D, BASE_SEED, row0=off)
+        rows = torch.zeros((N + 1, dp), dtype=torch.float32, device=dev)
+        rows[1:, :D] = torch.from_numpy(base).to(dev)
+        ix = DeviceIndex("l2", "float", D, device=local)
+        ix.set_objects_device(rows.data_ptr(), N + 1)
+        offsets, edges = build_graph(torch, rows[1:, :D], args.knn, args.out_deg, args.in_deg, args.max_deg, dev)
+        ix.set_search_property(0, 30, 20, args.seed_size, 0)
+        ix.set_graph_device(offsets.data_ptr(), edges.data_ptr(), edges.numel())
+        sh = {"ix": ix, "rows": rows, "offsets": offsets, "edges": edges, "off": off, "qg_local": None}
+        if qgm:
+            # ngtqg quantize of this shard: kmeansWithNGT codebooks from its
+            # first 1,600 objects, encoder, quantized graph (QuantizedGraph.h:456-475)
+            h_base = np.zeros((min(N, 1600) + 1, D), np.float32)
+            h_base[1:] = base[:min(N, 1600)]
+            sh["qg_local"] = ix.qg_train_ngt(h_base, dsub=1)
+            ix.qg_encode(return_codes=False)
+            ix.qg_build_graph(None, args.qg_edges)
+        del base
+        shards.append(sh)
+        torch.cuda.synchronize()
+        log("shard %d/%d (offset %d) ready at %.1f s" % (s + 1, S, off, time.time() - t0))
+    setup_s = time.time() - t0
+    ix0 = shards[0]["ix"]
+    main = torch.cuda.current_stream(dev)
+    qraw = torch.from_numpy(qry).to(dev)
+    qdev = torch.zeros((NQ, dp), dtype=torch.float32, device=dev)
+    ix0.prepare_queries_device(qraw.data_ptr(), NQ, qdev.data_ptr(), stream=main.cuda_stream)
+    sx = ShardedIndex(torch, dist, [sh["ix"] for sh in shards], [sh["off"] for sh in shards], dev)
+
+    def buffers():
+        return (torch.zeros((S, NQ, K), dtype=torch.int32, device=dev),
+                torch.zeros((S, NQ, K), dtype=torch.float32, device=dev),
+                torch.zeros((S, NQ), dtype=torch.int32, device=dev))
+
+    # exact ground truth of the whole index: every shard's linear search, merged
+    t1 = time.time()
+    gi, gd, gn = buffers()
+    for s, sh in enumerate(shards):
+        sh["ix"].linear_search_device(qdev.data_ptr(), dp * 4, NQ, K, gi[s].data_ptr(), gd[s].data_ptr(),
+                                      gn[s].data_ptr(), stream=main.cuda_stream)
+    gt = sx.merge_local(gi, gd, gn, K, main.cuda_stream)[0].cpu().numpy()
+    del gi, gd, gn
+    log("ground truth (%d shard scans + merge) in %.1f s" % (S * world, time.time() - t1))
+
+    seeds = random_seeds(N + 1, NQ, args.seed_size)
+    d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
+    d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * args.seed_size
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    out_i, out_d, out_n = buffers()
+    cnt = torch.zeros((S, NQ, COUNTERS), dtype=torch.int64, device=dev)
+    merged = {}
+
+    def search_shard(s, eps, st, visited):
+        ix = shards[s]["ix"]
+        if qgm:
+            ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, out_i[s].data_ptr(), out_d[s].data_ptr(),
+                                out_n[s].data_ptr(), cnt[s].data_ptr(), k=K, epsilon=eps,
+                                result_expansion=args.expansion, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                                d_seed_off=d_soff.data_ptr(), stream=st, visited_hash_log2=visited)
+        else:
+            ix.search_device(qdev.data_ptr(), dp * 4, NQ, out_i[s].data_ptr(), out_d[s].data_ptr(),
+                             out_n[s].data_ptr(), cnt[s].data_ptr(), k=K, epsilon=eps, edge_size=0,
+                             seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
+                             stream=st, visited_hash_log2=visited)
+
+    def run(eps, visited=None):
+        visited = args.visited if visited is None else visited
+        # the shard streams wait for the previous step's pack (it reads out_*)
+        for st in streams:
+            st.wait_stream(main)
+        for s in range(S):
+            search_shard(s, eps, streams[s].cuda_stream, visited)
+        for st in streams:
+            main.wait_stream(st)
+        merged["r"] = sx.merge_local(out_i, out_d, out_n, K, main.cuda_stream)
+
+    sweep = []
+
+    def measure(eps):
+        run(eps)
+        torch.cuda.synchronize()
+        r = recall_at(merged["r"][0].cpu().numpy(), gt, K)
+        sweep.append((round(eps, 5), r, None, NQ))
+        log("eps %.4f merged recall@%d %.4f" % (eps, K, r))
+        return r
+
+    chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None)
+    rec = measure(chosen)
+    for _ in range(20):
+        if rec >= args.target or args.eps:
+            break
+        chosen = round(chosen * 1.02 + 1e-4, 5)
+        rec = measure(chosen)
+    for _ in range(max(1, args.warmup)):
+        run(chosen)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        run(chosen)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t1
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    qps = NQ * args.steps / elapsed
+    res = [x.clone() for x in merged["r"]]
+    # per-launch kernel time: each shard's search alone on the main stream
+    kms = []
+    for s in range(S):
+        search_shard(s, chosen, main.cuda_stream, args.visited)
+        torch.cuda.synchronize()
+        kms.append(shards[s]["ix"].last_search_kernel_ms())
+    filtered = (not qgm) and ix0.last_search_filtered()
+    if not qgm and args.visited == -2:
+        # the reference's distinct distance counts (every evaluated id in the
+        # visited set) for the algorithmic bytes; the results must not change
+        run(chosen, visited=-1)
+        torch.cuda.synchronize()
+        same = all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip(res, merged["r"]))
+        if not same:
+            raise SystemExit("bench: accepted-only visited set changed the merged results")
+    c = cnt.cpu().numpy().astype(np.float64).reshape(S * NQ, COUNTERS)
+    if qgm:
+        me = (D + 1) // 2 * 2
+        alg_bytes = (c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4
+                     + S * NQ * (dp * 4 + K * 8))
+        kname = "ngt_qg_search_kernel"
+    elif filtered:
+        alg_bytes = ((c[:, 0] - c[:, 7]).sum() * dp + (c[:, 7] + c[:, 6]).sum() * dp * 4 + c[:, 4].sum() * 4
+                     + S * NQ * (dp * 4 + K * 8))
+        kname = "ngt_graph_search_kernel"
+    else:
+        alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + S * NQ * (dp * 4 + K * 8)
+        kname = "ngt_graph_search_kernel"
+    kernel_ms = float(np.mean(kms))
+    per_launch = alg_bytes / S
+    achieved = per_launch / (kernel_ms * 1e-3) / 1e9
+
+    cpu = parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, parity = shard_parity_sample(args, shards, qdev, seeds, chosen, res, qgm)
+
+    if rank == 0:
+        total = N * S * world
+        if qgm:
+            metric_name = "QPS at recall@10=0.95, %d x %d-d NGTQG sharded over %d GPUs" % (total, D, world)
+            workload = ("C5 form: %d objects per GPU as %d NGTQG shards of %d (dsub=1, M=%d, result_expansion %g), "
+                        "%d GPUs, %d queries/step over all shards, k=%d, one packed RCCL all-gather of per-shard "
+                        "top-k + device merge" % (N * S, S, N, D, args.expansion, world, NQ, K))
+        else:
+            metric_name = "QPS at recall@10=0.95, %d x %d-d float L2 sharded over %d GPUs" % (total, D, world)
+            workload = ("C4 form: %d objects per GPU as %d shards of %d, %d GPUs, %d queries/step over all shards, "
+                        "k=%d, one packed RCCL all-gather of per-shard top-k + device merge" % (
+                            N * S, S, N, world, NQ, K))
+        line = {
+            "metric": metric_name, "value": qps, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" if not qgm else "u4-adc/u8-lut/f32-rerank",
+            "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
+            "config": {"workload": workload, "objects_total": total, "shards_per_gpu": S, "objects_per_shard": N,
+                       "recall_at_10": rec, "epsilon": chosen,
+                       "graph": "kNN%d out%d in%d max%d per shard" % (args.knn, args.out_deg, args.in_deg,
+                                                                     args.max_deg),
+                       "seeds": "getRandomSeeds (%d)" % args.seed_size, "setup_s": setup_s,
+                       "distance_filter": "1-byte filter copy" if filtered else "none",
+                       "parallelism": "shards x%d (%d per GPU, one stream each)" % (S * world, S),
+                       "distance_computations_per_query_per_shard": float(c[:, 0].mean()),
+                       "expansions_per_query_per_shard": float(c[:, 2].mean())},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,
+                         "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": per_launch,
+                         "what": "one shard's search launch alone (mean over the %d local shards)" % S,
+                         "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
+                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS},
+            "cpu_baseline": cpu, "parity_sample": parity, "sweep": sweep}
+        if qgm:
+            line["config"]["result_expansion"] = args.expansion
+        print(json.dumps(line), file=result_out, flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):
+    """The first --shard-sample queries of the batch through the oracle on
+    every shard (searchReadOnlyGraph restatement, or the NGTQG search from the
+    oracle's own LUTs on the shard's codebooks), merged on the host by
+    (distance, global id): ids and float bits must equal the device's merged
+    results (abort otherwise).  Its time is the CPU baseline of the whole
+    sharded index on the host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    K = args.k
+    n = min(args.shard_sample, qdev.shape[0])
+    h_q = qdev[:n].cpu().numpy()
+    model, ncpu, threads = host_cpu()
+    isa = O.host_isa()
+    L = O.native_lib(isa)
+    el = 0.0
+    cand = [[] for _ in range(n)]
+    for sh in shards:
+        h_rows = sh["rows"].cpu().numpy()
+        h_off = sh["offsets"].cpu().numpy().astype(np.uint64)
+        h_edges = sh["edges"].cpu().numpy().astype(np.uint32)
+        if qgm:
+            ids, codes = sh["ix"].qg_get_graph()
+            deg = (ids != 0).sum(1).astype(np.uint64)
+            qoff = np.zeros(len(deg) + 1, np.uint64)
+            qoff[1:] = np.cumsum(deg)
+            qg = {"M": args.dim, "qids": ids[ids != 0].astype(np.uint32), "qoff": qoff,
+                  "code_off": np.arange(len(deg) + 1, dtype=np.uint64) * np.uint64(codes.shape[1]),
+                  "codes": np.ascontiguousarray(codes.reshape(-1))}
+            qgo = {"M": args.dim, "dim": args.dim, "dsub": 1, "global": np.zeros(args.dim, np.float32),
+                   "local": oracle_codebooks(sh["qg_local"])}
+            t0 = time.perf_counter()
+            lut, sc, to = qg_luts_oracle(O, qgo, h_q, n)
+            oi, od, on, _ = O.qg_search_batch(qg, h_rows, h_q, seeds[:n], K, eps, args.expansion, lut, sc, to,
+                                              threads=threads, L=L)
+        else:
+            t0 = time.perf_counter()
+            oi, od, on, _ = O.search_batch("l2", h_rows, h_off, h_edges, h_q, seeds[:n], K, np.float32(eps),
+                                           edge_size=0, threads=threads, L=L)
+        el += time.perf_counter() - t0
+        for q in range(n):
+            for j in range(int(on[q])):
+                cand[q].append((float(od[q, j]), int(oi[q, j]) + sh["off"], od[q, j]))
+        del h_rows, h_off, h_edges
+    gi = merged[0][:n].cpu().numpy().view(np.uint32)
+    gd = merged[1][:n].cpu().numpy()
+    gn = merged[2][:n].cpu().numpy()
+    same = True
+    for q in range(n):
+        best = sorted(cand[q], key=lambda t: (t[0], t[1]))[:K]
+        if int(gn[q]) != len(best) or any(int(gi[q, j]) != b[1] or gd[q, j].view(np.uint32) != b[2].view(np.uint32)
+                                          for j, b in enumerate(best)):
+            same = False
+            log("shard parity: query %d differs" % q)
+            break
+    parity = {"queries": n, "identical": same,
+              "checked": "merged ids and float32 distance bits vs the oracle on every shard + host merge"}
+    if not same:
+        raise SystemExit("bench: sharded results differ from the oracle: %s" % parity)
+    log("shard parity sample: %d queries identical to the oracle over %d shards (%.1f s on %d threads)" % (
+        n, len(shards), el, threads))
+    what = "NGTQG search restatement (oracle LUTs)" if qgm else "searchReadOnlyGraph restatement"
+    cpu = {"value": n / el, "unit": "queries/s", "cores": threads, "kind": "port",
+           "sample": "first %d queries over all %d local shards, oracle/ngt_oracle.c %s built -O3 -march=x86-64-%s, "
+                     "one query per thread per shard on %d threads, %.1f s; host: %s, %d CPUs" % (
+                         n, len(shards), what, isa, threads, el, model, ncpu)}
+    return cpu, parity
+
+
 def host_cpu():
     """lscpu's model name and CPU count, and the threads the baseline may use
     (the process's affinity, capped by OMP_NUM_THREADS when set)."""
@@ -997,6 +1320,16 @@ def scan_sample_check(rows, qdev, metric, k, gt_i, gt_d, gt_n, nsample=16):
     return {"queries": nsample, "identical": True}
 
 
+def oracle_codebooks(local):
+    """[M][16][dsub] centroids (local ids 1..16) -> the oracle's layout, the
+    local codebook index's object slots [M][17][dsub] with the dummy slot 0
+    (ObjectRepository.h:37-40; tests/golden/ngt_files.py read_qg)."""
+    M, _, dsub = local.shape
+    out = np.zeros((M, 17, dsub), np.float32)
+    out[:, 1:, :] = local
+    return out
+
+
 def qg_luts_oracle(O, qgo, h_q, n):
     luts, scs, tos = [], [], []
     for i in range(n):
@@ -1039,7 +1372,7 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
         # the LUTs from the oracle's createDistanceLookup (Quantizer.h:709-760)
         # on the same codebooks: the sample checks LUT + ADC + search
         qgo = {"M": args.dim, "dim": args.dim, "dsub": 1, "global": np.zeros(args.dim, np.float32),
-               "local": qg_local}
+               "local": oracle_codebooks(qg_local)}
         lut, sc, to = qg_luts_oracle(O, qgo, h_q, min(h_q.shape[0], 20000))
     log("cpu baseline: host copy %.1f s; %s, %d CPUs, %d threads, oracle %s build" % (
         time.time() - t0, model, ncpu, threads, isa))

@@ -597,6 +597,10 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     while ((1u << a.la_sh_log2) < sh_want) a.la_sh_log2++;
     if (a.vf_log2 == 0) a.vf_log2 = 15;
     a.cq_cap = la_mode == 0 ? 512u : 2048u;
+    if (la_mode == 0 && la_wpe() == 4) {
+      a.vf_log2 = 14;
+      a.cq_cap = 256u;
+    }
     if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
     if (const char* v = getenv("NGT_AMD_VFILTER"))
       if (atoi(v) > 0) a.vf_log2 = (uint32_t)std::max(11, std::min(18, atoi(v)));
@@ -613,8 +617,33 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     a.seed_off = d_seed_off;
   }
   const size_t lds_max = std::max<size_t>(64 * 1024, std::min<size_t>(ix->lds_per_block, ix->lds_per_cu));
-  if (la_mode >= 0 && search_la_lds_bytes(a, (int)la_targets(la_mode)) > lds_max) la_mode = -1;  // large k
-  const size_t lds = la_mode >= 0 ? search_la_lds_bytes(a, (int)la_targets(la_mode)) : search_lds_bytes(a, ix->otype);
+  // latency launches: the speculating kernel (search_lat.hip) when the exact
+  // LDS visited bitmap of every object fits one CU's LDS with its slots
+  bool lat = false;
+  if (la_mode == 1) {
+    static const bool lat_on = [] {
+      const char* v = getenv("NGT_AMD_LAT");
+      return v && atoi(v) != 0;  // opt-in until measured
+    }();
+    if (lat_on && a.adj) {
+      const uint32_t cap = (uint32_t)std::min<uint64_t>(a.adj_stride, a.edge_size);
+      SearchArgs b = a;
+      b.lat_slots = cap <= 64 ? 32u : 16u;
+      b.lat_tail = 4096u;
+      while (search_lat_lds_bytes(b) > lds_max && b.lat_tail > 512u) b.lat_tail -= 256u;
+      while (search_lat_lds_bytes(b) > lds_max && b.lat_slots > 8u) b.lat_slots -= 2u;
+      // test knobs: a small tail forces the HBM spill, few slots the orphan path
+      if (const char* v = getenv("NGT_AMD_LAT_TAIL")) b.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
+      if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) b.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
+      if (search_lat_lds_bytes(b) <= lds_max) {
+        a = b;
+        lat = true;
+      }
+    }
+  }
+  if (!lat && la_mode >= 0 && search_la_lds_bytes(a, (int)la_targets(la_mode)) > lds_max) la_mode = -1;  // large k
+  const size_t lds = lat ? search_lat_lds_bytes(a)
+                         : la_mode >= 0 ? search_la_lds_bytes(a, (int)la_targets(la_mode)) : search_lds_bytes(a, ix->otype);
   if (lds > lds_max) return fail("search: k=%u needs %zu bytes of LDS per query (max %zu)", a.k, lds, lds_max);
   if (ensure_vis_scratch(ix, c, lds, nq, s)) return -1;
   a.vis = c->vis.p;
@@ -628,7 +657,9 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   c->launch_slots = slots;
   c->launch_la = la_mode;
   HIP_OK(hipEventRecord(c->ev0, s));
-  if (la_mode >= 0) {
+  if (lat) {
+    HIP_OK(launch_graph_search_lat(a, slots, s));
+  } else if (la_mode >= 0) {
     // full visited set unless the caller asked for the accepted-only one
     HIP_OK(launch_graph_search_la(a, la_mode, !a.accepted_only, slots, s));
   } else {

@@ -92,6 +92,9 @@ struct SearchArgs {
   // target lists, >= 256) and log2 of the per-step id hash (>= log2(2 lmax))
   uint32_t la_lmax;
   uint32_t la_sh_log2;
+  // latency kernel (search_lat.hip): speculation slots and LDS tail keys
+  uint32_t lat_slots;
+  uint32_t lat_tail;
 };
 
 // lookahead targets per step of search_la.hip: mode 0 (throughput, one wave
@@ -101,7 +104,19 @@ inline uint32_t la_targets(int mode) {
   const char* v = getenv("NGT_AMD_LA_P");  // 3 (default: fewer discarded targets per step) or 4
   return v && atoi(v) == 4 ? 4u : 3u;
 }
+// resident waves per SIMD of the throughput form: 3 (168 VGPRs, 6 filter
+// groups in flight, 512 LDS keys, 32 Kbit filter) or 4 (128 VGPRs, 4 groups,
+// 256 keys, 16 Kbit: <= 10 KB of LDS so 16 workgroups fit a CU)
+inline int la_wpe() {
+  static const int w = [] {
+    const char* v = getenv("NGT_AMD_LA_WPE");
+    return v && atoi(v) == 4 ? 4 : 3;
+  }();
+  return w;
+}
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
+uint32_t search_lat_lds_bytes(const SearchArgs& a);
+hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStream_t s);
 hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint32_t slots, hipStream_t s);
 
 struct LinearArgs {

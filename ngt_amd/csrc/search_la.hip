@@ -47,7 +47,7 @@ struct LaCtl {
 
 // 16-byte aligned LDS carve-out; the host's search_la_lds_bytes mirrors it.
 struct LaLayout {
-  uint32_t off_tkey, off_tcnt, off_loff, off_xoff, off_vf, off_cq, off_cmin, off_res, off_q, off_qb, off_l,
+  uint32_t off_tkey, off_tcnt, off_loff, off_xoff, off_vf, off_cq, off_res, off_q, off_qb, off_l,
       off_lfl, off_x, off_xd, off_sh, off_nid, off_nd, total;
   __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
   __host__ __device__ LaLayout(const SearchArgs& a, int P) {
@@ -58,7 +58,6 @@ struct LaLayout {
     off_xoff = o; o = up16(o + 4u * (P + 1));
     off_vf = o; o = up16(o + ((1u << a.vf_log2) >> 3));
     off_cq = o; o = up16(o + 8u * a.cq_cap);
-    off_cmin = o; o = up16(o + 8u * ((a.cq_cap + 63) / 64));
     off_res = o; o = up16(o + 8u * (a.k + 1));
     off_q = o; o = up16(o + 4u * (uint32_t)a.dp);
     off_qb = o; o = up16(o + (uint32_t)a.dp);
@@ -100,9 +99,16 @@ __device__ __forceinline__ bool vf_test(const uint32_t* vf, uint32_t shift, uint
   return (vf[b >> 5] >> (b & 31)) & 1u;
 }
 
-// W = 1: three waves per SIMD (<= 168 VGPRs; the LDS allows ~10 waves per CU)
-template <int NCH, int W, int PW, int RG, int EG, bool FULL>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 3 : 2)))
+// a wave-uniform u64 in SGPRs (the reductions leave it in every lane)
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// WPE: resident waves per SIMD the kernel is compiled for (VGPR budget)
+template <int NCH, int W, int PW, int RG, int EG, bool FULL, int WPE>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
 ngt_graph_search_la_kernel(SearchArgs a) {
   constexpr int P = W * PW;
   constexpr int E = 4 * NCH;  // filter-code bytes per lane of a quad
@@ -117,7 +123,6 @@ ngt_graph_search_la_kernel(SearchArgs a) {
   uint32_t* xoff = reinterpret_cast<uint32_t*>(smem + lay.off_xoff);
   uint32_t* vf = reinterpret_cast<uint32_t*>(smem + lay.off_vf);
   uint64_t* cq = reinterpret_cast<uint64_t*>(smem + lay.off_cq);
-  uint64_t* cmin = reinterpret_cast<uint64_t*>(smem + lay.off_cmin);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + lay.off_res);
   float* qlds = reinterpret_cast<float*>(smem + lay.off_q);
   uint8_t* qb = smem + lay.off_qb;
@@ -172,6 +177,14 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     uint32_t ncq = 0, nspill = 0, nres = 0, maxq = 0;
     uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, ndisc = 0, ns = 0;
     uint32_t sh_used = 0;  // ids inserted into this step's id set
+    // wave 0's copy of the step's targets (ascending keys, compile-time indexed)
+    // and the commit guard: nblock = the first target j > 0 that a key pushed
+    // by this step's earlier commits precedes (that key, not t_j, is then the
+    // reference's next pop)
+    uint64_t tk[P];
+#pragma unroll
+    for (int j = 0; j < P; j++) tk[j] = ~0ull;
+    uint32_t nt0 = 0, nblock = P, cur_j = 0;
     // diagnostic build only: shader-clock totals per phase (wave 0's view)
     uint64_t t_a = 0, t_b = 0, t_c = 0, t_e = 0, t_f = 0, t_last = 0, nsteps = 0;
     (void)t_a; (void)t_b; (void)t_c; (void)t_e; (void)t_f; (void)t_last; (void)nsteps;
@@ -180,22 +193,13 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     double frq = 0.0;
     // ---- the unchecked set: two levels with a key threshold T ------------
     // LDS keys are all < T <= every spill key (HBM, per slot), so the
-    // minimum is always in LDS while LDS is non-empty (chunk minima, no
-    // spill scan).  A full LDS is compacted (keys beyond the exploration
-    // radius can never be popped, Graph.cpp:433-435) and, if still over
-    // half full, its larger half moves to the spill (T drops); an empty LDS
-    // refills with the smallest spill keys (T rises).  Exact throughout.
+    // smallest keys are always in LDS while LDS is non-empty (no spill
+    // scan).  A full LDS is compacted (keys beyond the exploration radius can
+    // never be popped, Graph.cpp:433-435) and, if still over half full, its
+    // larger half moves to the spill (T drops); an empty LDS refills with
+    // the smallest spill keys (T rises).  Exact throughout.  The LDS keys are
+    // unsorted: a step's targets come from one scan of them (phase A).
     uint64_t T = ~0ull;
-    auto chunk_min = [&](uint32_t c) {
-      const uint32_t i = 64 * c + (uint32_t)lane;
-      const uint64_t mn = wave_min_u64(i < ncq ? cq[i] : ~0ull);
-      if (lane == 0) cmin[c] = mn;
-    };
-    auto all_chunk_min = [&]() {
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t c = 0; c < ((ncq + 63) >> 6); c++) chunk_min(c);
-      __builtin_amdgcn_wave_barrier();
-    };
     auto spill_push = [&](uint64_t key) {
       if (nspill >= a.spill_cap) {
         if (lane == 0) atomicOr(a.error, 1);
@@ -258,7 +262,6 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         }
         lds_to_spill(l);
       }
-      all_chunk_min();
     };
     // refill an empty LDS with the smallest spill keys within the radius
     auto refill = [&]() {
@@ -331,7 +334,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       }
       nspill = out;
       T = nspill ? ((uint64_t)bound << 32) : ~0ull;
-      all_chunk_min();
+      __builtin_amdgcn_wave_barrier();
     };
     auto insert_key = [&](uint64_t key) {
       if (key >= T) {
@@ -341,47 +344,28 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if (key >= T) {
           spill_push(key);
         } else {
-          if (lane == 0) {
-            cq[ncq] = key;
-            const uint32_t c = ncq >> 6;
-            cmin[c] = (ncq & 63) == 0 ? key : (key < cmin[c] ? key : cmin[c]);
-          }
+          if (lane == 0) cq[ncq] = key;
           ncq++;
         }
       }
       if (ncq + nspill > maxq) maxq = ncq + nspill;
       __builtin_amdgcn_wave_barrier();
     };
-    // the minimum of the unchecked set (and its LDS chunk)
-    auto find_min = [&](uint32_t& bidx) -> uint64_t {
-      if (ncq == 0 && nspill != 0) refill();
-      uint64_t best = ~0ull;
-      bidx = 0xffffffffu;
-      const uint32_t nch = (ncq + 63) >> 6;
-      if ((uint32_t)lane < nch) { best = cmin[lane]; bidx = (uint32_t)lane; }
-      if ((uint32_t)lane + 64 < nch) {
-        const uint64_t v = cmin[lane + 64];
-        if (v < best) { best = v; bidx = (uint32_t)lane + 64; }
-      }
-      const uint64_t wbest = wave_min_u64(best);
-      const uint64_t owner = ballot64(best == wbest);
-      bidx = __shfl(bidx, __ffsll((long long)owner) - 1, 64);
-      return wbest;
+    // keys entering the unchecked set during the commit of target cur_j: the
+    // first later target they precede can no longer be the reference's next
+    // pop (targets ascend, so every later one is blocked too)
+    auto note_pushed = [&](bool mine, uint64_t key) {
+#pragma unroll
+      for (int jj = 1; jj < P; jj++)
+        if ((uint32_t)jj > cur_j && (uint32_t)jj < nblock && ballot64(mine && key < tk[jj]) != 0ull)
+          nblock = (uint32_t)jj;
     };
-    // remove the minimum found by find_min; false on a stale chunk minimum
-    auto remove_min = [&](uint64_t wbest, uint32_t bidx) -> bool {
-      const uint32_t i = 64 * bidx + (uint32_t)lane;
-      const uint64_t in = ballot64(i < ncq && cq[i] == wbest);
-      if (in == 0) return false;
-      bidx = 64 * bidx + (uint32_t)(__ffsll((long long)in) - 1);
-      if (lane == 0) cq[bidx] = cq[ncq - 1];
-      __builtin_amdgcn_wave_barrier();
-      ncq--;
-      const uint32_t c0 = bidx >> 6, c1 = ncq >> 6;
-      chunk_min(c0);
-      if (c1 != c0) chunk_min(c1);
-      __builtin_amdgcn_wave_barrier();
-      return true;
+    auto tk_at = [&](uint32_t j) -> uint64_t {
+      uint64_t r = tk[0];
+#pragma unroll
+      for (int jj = 1; jj < P; jj++)
+        if ((uint32_t)jj == j) r = tk[jj];
+      return r;
     };
     // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
     // order (Graph.cpp:471-483); only candidates within the radius at batch
@@ -404,13 +388,11 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         }
         sh_used += cnt;
       }
+      note_pushed(mine, key);
       const bool below = ballot64(mine && key >= T) == 0ull;
       if (below && ncq + cnt <= a.cq_cap) {
-        const uint32_t n0 = ncq;
-        if (mine) cq[n0 + mbcnt(bm)] = key;
+        if (mine) cq[ncq + mbcnt(bm)] = key;
         ncq += cnt;
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t c = n0 >> 6; c <= (ncq - 1) >> 6; c++) chunk_min(c);
         __builtin_amdgcn_wave_barrier();
         if (ncq + nspill > maxq) maxq = ncq + nspill;
       } else {
@@ -452,6 +434,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           }
           sh_used++;
         }
+        note_pushed(true, key);
         insert_key(key);
         res_insert(res, nres, k, key);
         if (nres >= k) {
@@ -503,51 +486,78 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     t_last = stamp();
 #endif
     for (;;) {
-      // A. wave 0: pop the reference's next node, pick the next keys in line
+      // A. wave 0: the reference's next pop and the keys in line after it --
+      // the nt <= P smallest keys of the unchecked set within the exploration
+      // radius (all in LDS: spill keys are >= T > every LDS key).  Every lane
+      // keeps the two smallest keys of its share (with positions), the wave
+      // takes the minimum of the lanes' heads nt times, and a lane that runs
+      // out of heads rescans its share above the last key it gave.  The
+      // targets leave the LDS array now; those the commit does not reach go
+      // back at the end of the step.
       if (wave == 0) {
-        uint32_t bidx;
-        const uint64_t key = find_min(bidx);
-        uint32_t done = 0, nt = 0;
-        if (key == ~0ull || key_dist(key) > expr) {
-          done = 1;
-        } else if (!remove_min(key, bidx)) {
-          if (lane == 0) atomicOr(a.error, 4);  // stale chunk minimum: never expected
-          done = 1;
-        } else {
-          if (lane == 0) tkey[0] = key;
-          nt = 1;
-          if constexpr (P > 1) {
-            // the next P - 1 keys in line (all LDS keys are > key; spill keys
-            // are larger still): every lane keeps its two smallest keys, the
-            // wave takes the minimum of the lanes' heads P - 1 times, and a
-            // lane that runs out of heads rescans its share above the last
-            // key it gave
-            uint64_t h0 = ~0ull, h1 = ~0ull;
-            for (uint32_t i = lane; i < ncq; i += 64) {
-              const uint64_t v = cq[i];
-              if (v < h1) {
-                if (v < h0) { h1 = h0; h0 = v; } else { h1 = v; }
-              }
+        if (ncq == 0 && nspill != 0) refill();
+        uint32_t nt = 0;
+        uint32_t tix[P];
+        {
+          uint64_t h0 = ~0ull, h1 = ~0ull;
+          uint32_t i0 = 0, i1 = 0;
+          for (uint32_t i = lane; i < ncq; i += 64) {
+            const uint64_t v = cq[i];
+            if (v < h1) {
+              if (v < h0) { h1 = h0; i1 = i0; h0 = v; i0 = i; } else { h1 = v; i1 = i; }
             }
-            for (int j = 1; j < P; j++) {
-              const uint64_t m = wave_min_u64(h0);
-              if (m == ~0ull || key_dist(m) > expr) break;
-              if (lane == 0) tkey[j] = m;
-              nt++;
-              if (h0 == m) {  // keys are distinct: one owner
-                h0 = h1;
-                h1 = ~0ull;
-                if (h0 == ~0ull) {
-                  for (uint32_t i = lane; i < ncq; i += 64) {
-                    const uint64_t v = cq[i];
-                    if (v > m && v < h1) {
-                      if (v < h0) { h1 = h0; h0 = v; } else { h1 = v; }
-                    }
+          }
+#pragma unroll
+          for (int j = 0; j < P; j++) {
+            tk[j] = ~0ull;
+            tix[j] = 0u;
+            if ((uint32_t)j != nt) continue;  // an earlier key ended the list
+            const uint64_t m = uniform_u64(wave_min_u64(h0));
+            if (m == ~0ull || key_dist(m) > expr) continue;
+            const int ol = __ffsll((long long)ballot64(h0 == m)) - 1;  // keys are distinct: one owner
+            tk[j] = m;
+            tix[j] = (uint32_t)__builtin_amdgcn_readlane((int)i0, ol);
+            nt++;
+            if (j + 1 < P && lane == ol) {
+              h0 = h1;
+              i0 = i1;
+              h1 = ~0ull;
+              if (h0 == ~0ull) {
+                for (uint32_t i = lane; i < ncq; i += 64) {
+                  const uint64_t v = cq[i];
+                  if (v > m && v < h1) {
+                    if (v < h0) { h1 = h0; i1 = i0; h0 = v; i0 = i; } else { h1 = v; i1 = i; }
                   }
                 }
               }
             }
           }
+        }
+        // swap-remove the targets, highest position first (a moved tail key
+        // is never a target still to remove)
+#pragma unroll
+        for (int x = 0; x < P; x++)
+#pragma unroll
+          for (int y = x + 1; y < P; y++)
+            if (tix[y] > tix[x] && (uint32_t)y < nt) {
+              const uint32_t t = tix[x];
+              tix[x] = tix[y];
+              tix[y] = t;
+            }
+#pragma unroll
+        for (int x = 0; x < P; x++) {
+          if ((uint32_t)x < nt) {
+            if (lane == 0) cq[tix[x]] = cq[ncq - 1];
+            __builtin_amdgcn_wave_barrier();
+            ncq--;
+          }
+        }
+        nt0 = nt;
+        const uint32_t done = nt == 0 ? 1u : 0u;  // empty, or the minimum is beyond the radius (Graph.cpp:433-435)
+        if (lane == 0) {
+#pragma unroll
+          for (int j = 0; j < P; j++)
+            if ((uint32_t)j < nt) tkey[j] = tk[j];
         }
         if (lane == 0) {
           ctl->done = done;
@@ -742,35 +752,29 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       __syncthreads();
       NGT_MARK(t_e);
 
-      // F. wave 0 commits in the reference's pop order
+      // F. wave 0 commits in the reference's pop order.  After commits
+      // 0..j-1 the unchecked set is the step-start set minus t_0..t_{j-1}
+      // plus the keys those commits pushed; its minimum is t_j unless one of
+      // the pushed keys precedes it (nblock <= j: speculation ends, that key
+      // is the next pop), and the reference stops when that minimum lies
+      // beyond the exploration radius (Graph.cpp:433-435).
       if (wave == 0) {
-        uint32_t done = 0;
+        uint32_t done = 0, ncommit = 0;
         sh_used = 0;
+        nblock = P;
         for (uint32_t j = 0; j < ntl_s; j++) {
+          cur_j = j;
           if (j > 0) {
             // the step's id set must never fill: stop before a target whose
             // every entry could be inserted would pass half its capacity
-            if (sh_used + (loff[j + 1] - loff[j]) > sh_n / 2) {
-              ndisc += ntl_s - j;
-              break;
-            }
-            uint32_t bidx;
-            const uint64_t m = find_min(bidx);
-            if (m == ~0ull || key_dist(m) > expr) {  // the reference stops here (Graph.cpp:433-435)
-              done = 1;
-              ndisc += ntl_s - j;
-              break;
-            }
-            if (m != tkey[j]) {  // something closer was accepted: speculation ends
-              ndisc += ntl_s - j;
-              break;
-            }
-            if (!remove_min(m, bidx)) {
-              if (lane == 0) atomicOr(a.error, 4);
+            if (sh_used + (loff[j + 1] - loff[j]) > sh_n / 2) break;
+            if (nblock <= j) break;
+            if (key_dist(tk_at(j)) > expr) {
               done = 1;
               break;
             }
           }
+          ncommit++;
           nexp++;
           const uint32_t lb = loff[j], le = loff[j + 1];
           nedge += le - lb;
@@ -807,7 +811,13 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             __builtin_amdgcn_wave_barrier();
           }
         }
-        if (lane == 0 && done) ctl->done = 1;
+        ndisc += ntl_s - ncommit;
+        if (done) {
+          if (lane == 0) ctl->done = 1;
+        } else {
+          // the targets the commit did not reach return to the unchecked set
+          for (uint32_t j = ncommit; j < nt0; j++) insert_key(tk_at(j));
+        }
       }
       __syncthreads();
       NGT_MARK(t_f);
@@ -857,38 +867,39 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
   if (a.dp != 128 && a.dp != 96) return hipErrorNotSupported;
   const uint32_t P = la_targets(mode);
   const size_t lds = search_la_lds_bytes(a, (int)P);
-#define LA(NCH, W, PW, RG, EG, F)                                                                              \
+#define LA(NCH, W, PW, RG, EG, F, WPE)                                                                         \
   do {                                                                                                          \
-    auto kern = ngt_graph_search_la_kernel<NCH, W, PW, RG, EG, F>;                                              \
+    auto kern = ngt_graph_search_la_kernel<NCH, W, PW, RG, EG, F, WPE>;                                         \
     if (lds > 64 * 1024) {                                                                                       \
       hipError_t e_ = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
       if (e_ != hipSuccess) return e_;                                                                          \
     }                                                                                                           \
     hipLaunchKernelGGL(kern, dim3(slots), dim3(64 * W), lds, s, a);                                             \
   } while (0)
+#define LA_T(NCH, PW)                                                                                           \
+  do {                                                                                                          \
+    if (la_wpe() == 4) {                                                                                        \
+      if (full) LA(NCH, 1, PW, 4, 1, true, 4); else LA(NCH, 1, PW, 4, 1, false, 4);                             \
+    } else {                                                                                                    \
+      if (full) LA(NCH, 1, PW, 6, 1, true, 3); else LA(NCH, 1, PW, 6, 1, false, 3);                             \
+    }                                                                                                           \
+  } while (0)
   if (mode == 0) {
     if (P == 3) {
-      if (a.dp == 128) {
-        if (full) LA(8, 1, 3, 6, 1, true); else LA(8, 1, 3, 6, 1, false);
-      } else {
-        if (full) LA(6, 1, 3, 6, 1, true); else LA(6, 1, 3, 6, 1, false);
-      }
+      if (a.dp == 128) LA_T(8, 3); else LA_T(6, 3);
     } else {
-      if (a.dp == 128) {
-        if (full) LA(8, 1, 4, 6, 1, true); else LA(8, 1, 4, 6, 1, false);
-      } else {
-        if (full) LA(6, 1, 4, 6, 1, true); else LA(6, 1, 4, 6, 1, false);
-      }
+      if (a.dp == 128) LA_T(8, 4); else LA_T(6, 4);
     }
   } else {
     // latency form: one workgroup per CU, 2 waves per SIMD -> room for 192
     // filter rows in flight per wave (1,536 per step's round trip)
     if (a.dp == 128) {
-      if (full) LA(8, 8, 1, 12, 1, true); else LA(8, 8, 1, 12, 1, false);
+      if (full) LA(8, 8, 1, 12, 1, true, 2); else LA(8, 8, 1, 12, 1, false, 2);
     } else {
-      if (full) LA(6, 8, 1, 12, 1, true); else LA(6, 8, 1, 12, 1, false);
+      if (full) LA(6, 8, 1, 12, 1, true, 2); else LA(6, 8, 1, 12, 1, false, 2);
     }
   }
+#undef LA_T
 #undef LA
   return hipGetLastError();
 }

@@ -36,12 +36,15 @@ def shard_bounds(n_total, world, rank):
 
 
 def gather_offsets(torch, dist, offset, device):
-    """All ranks' shard offsets, in rank order."""
+    """All ranks' shard offsets, in rank order; `offset` is this rank's offset
+    or the list of its local shards' offsets (the same count on every rank),
+    and the result lists every shard rank-major."""
     world = dist.get_world_size()
-    t = torch.tensor([offset], dtype=torch.int64, device=device)
+    local = list(offset) if isinstance(offset, (list, tuple)) else [offset]
+    t = torch.tensor(local, dtype=torch.int64, device=device)
     out = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(out, t)
-    return [int(x.item()) for x in out]
+    return [int(v) for x in out for v in x.tolist()]
 
 
 def pack_device(torch, ids, dists, n, k, stream=None):
@@ -57,12 +60,14 @@ def pack_device(torch, ids, dists, n, k, stream=None):
 
 
 def exchange_packed(torch, dist, packed):
-    """The one collective: all-gather of every rank's [nq, k] packed words ->
-    [world, nq, k] on every rank."""
+    """The one collective: all-gather of every rank's packed words, [nq, k]
+    (one shard per rank) or [S, nq, k] (S local shards) -> [world * S, nq, k]
+    on every rank, shards rank-major."""
     world = dist.get_world_size()
-    g = torch.empty((world * packed.shape[0],) + tuple(packed.shape[1:]), dtype=packed.dtype, device=packed.device)
-    dist.all_gather_into_tensor(g, packed.contiguous())
-    return g.view((world,) + tuple(packed.shape))
+    shape = tuple(packed.shape) if packed.dim() == 3 else (1,) + tuple(packed.shape)
+    g = torch.empty((world * shape[0] * shape[1], shape[2]), dtype=packed.dtype, device=packed.device)
+    dist.all_gather_into_tensor(g, packed.contiguous().view(shape[0] * shape[1], shape[2]))
+    return g.view((world * shape[0],) + shape[1:])
 
 
 def merge_packed_device(torch, g_packed, offsets, k, stream=None):
@@ -101,10 +106,16 @@ def merge_device(torch, g_ids, g_d, g_n, offsets, k, stream=None):
 
 class ShardedIndex(object):
     """Search front end of one rank's shard.  `index` is the rank's
-    DeviceIndex (ids 1..n_r local); `offset` its global id offset."""
+    DeviceIndex (ids 1..n_r local); `offset` its global id offset.  A rank may
+    also hold S shards (lists of S indexes and S offsets, the same S on every
+    rank): an index larger than one graph a run can build is served as S
+    shards per GPU -- each searched on its own stream, all S packed into the
+    rank's one all-gather message, and the merge ranks world * S lists."""
 
     def __init__(self, torch, dist, index, offset, device, pack=pack_device, merge=merge_packed_device):
-        self.torch, self.dist, self.index = torch, dist, index
+        self.torch, self.dist = torch, dist
+        self.indexes = list(index) if isinstance(index, (list, tuple)) else [index]
+        self.index = self.indexes[0]
         self.device = device
         self.offsets = gather_offsets(torch, dist, offset, device)
         self.pack = pack
@@ -128,7 +139,8 @@ class ShardedIndex(object):
 
     def merge_local(self, ids, dists, n, k, stream=None):
         """Pack, exchange (one all-gather) and merge already computed local
-        results (tensors [nq, k], [nq, k], [nq], written on `stream`).  The
+        results (tensors [nq, k], [nq, k], [nq] -- or [S, nq, k], [S, nq, k],
+        [S, nq] for S local shards -- written on `stream`).  The
         packed words, the gathered buffer and the merged outputs are allocated
         with `stream` current, so their zero-fills, the pack, the collective
         and the merge are all ordered on it; the inputs are recorded on it so
@@ -139,7 +151,10 @@ class ShardedIndex(object):
             if st is not None:
                 for x in (ids, dists, n):
                     x.record_stream(st)
-            packed = self.pack(t, ids, dists, n, k, stream)
+            if ids.dim() == 3:
+                packed = t.stack([self.pack(t, ids[s], dists[s], n[s], k, stream) for s in range(ids.shape[0])])
+            else:
+                packed = self.pack(t, ids, dists, n, k, stream)
             g = exchange_packed(t, self.dist, packed)
             return self.merge(t, g, self.offsets, k, stream)
 

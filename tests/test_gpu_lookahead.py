@@ -126,3 +126,36 @@ def test_lookahead_equals_single_expansion_kernel(monkeypatch, name):
             for c in (0, 2, 4):
                 assert np.array_equal(a[3][:, c], b[3][:, c]), (nq, eps, c)
     ix.close()
+
+
+@pytest.mark.parametrize("knobs", [{"NGT_AMD_LAT_TAIL": "128"}, {"NGT_AMD_LAT_SLOTS": "2"},
+                                   {"NGT_AMD_LAT_SLOTS": "3", "NGT_AMD_LAT_TAIL": "256"}])
+@pytest.mark.parametrize("deg", [24, 150])
+def test_latency_kernel_spill_and_slots(monkeypatch, knobs, deg):
+    """The speculating latency kernel (search_lat.hip) with a tail small
+    enough to push keys to the HBM spill and refill from it, and with so few
+    speculation slots that head entries lose theirs (orphaned slots reaped):
+    ids, distance bits and the reference's distance/expansion counts."""
+    for kv in knobs.items():
+        monkeypatch.setenv(*kv)
+    monkeypatch.setenv("NGT_AMD_LA", "2")
+    n, dim = 5000, 128
+    rows, offs, edges = _graph(n, dim, deg, 77 + deg)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(deg)
+    qs = rng.random((12, dim), dtype=np.float32)
+    seeds = [rng.choice(np.arange(1, n), 10, replace=False).astype(np.uint32) for _ in range(12)]
+    for eps in (0.1, 0.5):
+        gi, gd, gn, cnt = ix.search(qs, k=30, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN, seeds=seeds)
+        assert ix.last_search_lookahead() == 1
+        oi, od, on, oc = O.search_batch("l2", rows, offs, edges, qs, seeds, 30, np.float32(eps), edge_size=0,
+                                        threads=os.cpu_count() or 1)
+        assert np.array_equal(gn, on)
+        for i in range(12):
+            assert list(gi[i, :gn[i]]) == list(oi[i, :on[i]]), (eps, i)
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od[i, :on[i]].view(np.uint32)), (eps, i)
+        assert np.array_equal(cnt[:, 0], oc[:, 0].astype(np.uint64)), eps
+        assert np.array_equal(cnt[:, 2], oc[:, 2].astype(np.uint64)), eps
+    ix.close()

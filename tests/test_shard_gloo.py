@@ -60,7 +60,7 @@ def numpy_merge(torch, g_packed, offsets, k, stream=None):
     return out_i, out_d, out_n
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, per_rank=1):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -68,20 +68,34 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rows, qs = _data()
-        off, cnt = shard_bounds(N, world, rank)
-        shard = np.zeros((cnt + 1, DIM), np.float32)
-        shard[1:] = rows[off + 1:off + 1 + cnt]
-        ids = np.zeros((NQ, K), np.int32)
-        ds = np.zeros((NQ, K), np.float32)
-        n = np.zeros(NQ, np.int32)
-        for i in range(NQ):
-            oi, od = O.linear_search("l2", shard, qs[i], K)[:2]
-            n[i] = len(oi)
-            ids[i, :n[i]] = oi
-            ds[i, :n[i]] = od
-        sx = ShardedIndex(torch, dist, None, off, torch.device("cpu"), pack=numpy_pack, merge=numpy_merge)
-        gi, gd, gn = sx.merge_local(torch.from_numpy(ids), torch.from_numpy(ds), torch.from_numpy(n), K)
-        q.put((rank, off, cnt, sx.offsets, gi.numpy(), gd.numpy(), gn.numpy()))
+        # S = per_rank local shards: rank r holds shards r*S .. r*S+S-1
+        offs, all_ids, all_ds, all_n = [], [], [], []
+        for s in range(per_rank):
+            off, cnt = shard_bounds(N, world * per_rank, rank * per_rank + s)
+            shard = np.zeros((cnt + 1, DIM), np.float32)
+            shard[1:] = rows[off + 1:off + 1 + cnt]
+            ids = np.zeros((NQ, K), np.int32)
+            ds = np.zeros((NQ, K), np.float32)
+            n = np.zeros(NQ, np.int32)
+            for i in range(NQ):
+                oi, od = O.linear_search("l2", shard, qs[i], K)[:2]
+                n[i] = len(oi)
+                ids[i, :n[i]] = oi
+                ds[i, :n[i]] = od
+            offs.append(off)
+            all_ids.append(ids)
+            all_ds.append(ds)
+            all_n.append(n)
+        if per_rank == 1:
+            sx = ShardedIndex(torch, dist, None, offs[0], torch.device("cpu"), pack=numpy_pack, merge=numpy_merge)
+            gi, gd, gn = sx.merge_local(torch.from_numpy(all_ids[0]), torch.from_numpy(all_ds[0]),
+                                        torch.from_numpy(all_n[0]), K)
+        else:
+            sx = ShardedIndex(torch, dist, [None] * per_rank, offs, torch.device("cpu"), pack=numpy_pack,
+                              merge=numpy_merge)
+            gi, gd, gn = sx.merge_local(torch.from_numpy(np.stack(all_ids)), torch.from_numpy(np.stack(all_ds)),
+                                        torch.from_numpy(np.stack(all_n)), K)
+        q.put((rank, offs, None, sx.offsets, gi.numpy(), gd.numpy(), gn.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -104,12 +118,15 @@ def test_shard_bounds_partition():
 
 
 @pytest.mark.timeout(300)
-def test_sharded_search_equals_union_gloo():
+@pytest.mark.parametrize("per_rank", [1, 3])
+def test_sharded_search_equals_union_gloo(per_rank):
+    """world 2; per_rank 3: every rank holds three shards (C4/C5's index
+    served as several shards per GPU), six lists merged per query."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, per_rank)) for r in range(2)]
     for p in procs:
         p.start()
     import queue
@@ -128,7 +145,8 @@ def test_sharded_search_equals_union_gloo():
     assert len(outs) == 2
     outs.sort()
     rows, qs = _data()
-    assert outs[0][3] == outs[1][3] == [outs[0][1], outs[1][1]]
+    assert outs[0][3] == outs[1][3] == outs[0][1] + outs[1][1]
+    assert outs[0][3] == [shard_bounds(N, 2 * per_rank, s)[0] for s in range(2 * per_rank)]
     for rank, off, cnt, offsets, gi, gd, gn in outs:
         for i in range(NQ):
             oi, od = O.linear_search("l2", rows, qs[i], K)[:2]
