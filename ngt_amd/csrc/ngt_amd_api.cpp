@@ -623,7 +623,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   if (la_mode == 1) {
     static const bool lat_on = [] {
       const char* v = getenv("NGT_AMD_LAT");
-      return v && atoi(v) != 0;  // opt-in until measured
+      return !v || atoi(v) != 0;
     }();
     if (lat_on && a.adj) {
       const uint32_t cap = (uint32_t)std::min<uint64_t>(a.adj_stride, a.edge_size);

@@ -104,13 +104,14 @@ inline uint32_t la_targets(int mode) {
   const char* v = getenv("NGT_AMD_LA_P");  // 3 (default: fewer discarded targets per step) or 4
   return v && atoi(v) == 4 ? 4u : 3u;
 }
-// resident waves per SIMD of the throughput form: 3 (168 VGPRs, 6 filter
-// groups in flight, 512 LDS keys, 32 Kbit filter) or 4 (128 VGPRs, 4 groups,
-// 256 keys, 16 Kbit: <= 10 KB of LDS so 16 workgroups fit a CU)
+// resident waves per SIMD of the throughput form: 4 (128 VGPRs, 4 filter
+// groups in flight, 256 LDS keys, 16 Kbit filter: <= 10 KB of LDS so 16
+// workgroups fit a CU; ANNG 72.0k QPS) or 3 (168 VGPRs, 6 groups, 512 keys,
+// 32 Kbit; 64.7k QPS)
 inline int la_wpe() {
   static const int w = [] {
     const char* v = getenv("NGT_AMD_LA_WPE");
-    return v && atoi(v) == 4 ? 4 : 3;
+    return v && atoi(v) == 3 ? 3 : 4;
   }();
   return w;
 }

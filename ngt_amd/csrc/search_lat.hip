@@ -457,10 +457,19 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       };
       // hand a node to the speculation waves (they take the issued slot of
       // the smallest key first: the commit wave's next pops)
+      // every wait below is bounded: a slot that never becomes ready (never
+      // expected) flags error 16 and ends the query instead of hanging the CU
+      bool stuck = false;
       auto issue = [&](uint64_t key) -> uint32_t {
-        while (freem == 0ull) {
+        for (uint32_t spin = 0; freem == 0ull; spin++) {
           reap();
-          if (freem == 0ull) __builtin_amdgcn_s_sleep(1);
+          if (freem != 0ull) break;
+          if (spin > (1u << 24)) {
+            if (lane == 0) atomicOr(a.error, 16);
+            stuck = true;
+            return 0u;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
         const uint32_t s = (uint32_t)(__ffsll((long long)freem) - 1);
         freem &= ~(1ull << s);
@@ -478,6 +487,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           need &= need - 1;
           if (freem == 0ull) break;
           const uint32_t s = issue(readlane_u64(hk, l));
+          if (stuck) break;
           if (lane == l) ht = s;
         }
       };
@@ -557,8 +567,17 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           tag = issue(key);
           nwait++;
         }
+        if (stuck) break;
         feed();  // keep the speculation ahead while this node's list lands
-        while (lds_load_acq(&slots[tag].state) != kReady) __builtin_amdgcn_s_sleep(1);
+        for (uint32_t spin = 0; lds_load_acq(&slots[tag].state) != kReady; spin++) {
+          if (spin > (1u << 24)) {
+            if (lane == 0) atomicOr(a.error, 16);
+            stuck = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (stuck) break;
         const uint32_t n = slots[tag].n;
         nexp++;
         nedge += slots[tag].deg;
