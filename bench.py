@@ -583,11 +583,17 @@ def main():
                    "what": "one query per launch (nq=1), full visited set, device time incl. launch"}
         log("single-query launches: mean %.3f ms p50 %.3f p99 %.3f (lookahead form %d)" % (
             latency["mean_ms"], latency["p50_ms"], latency["p99_ms"], latency["form"]))
-        if "stamps" in os.environ.get("NGT_AMD_LIB", ""):
-            lcc = lc.cpu().numpy().astype(np.float64)
-            tot = lcc[:, [5, 6, 1, 7, 3]].mean(0)
-            log("single-query phase cycles: pop+targets %.3g adjacency %.3g filter %.3g exact %.3g commit %.3g "
-                "(sum %.3g); steps %.0f" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum(), lcc[:, 4].mean()))
+        lcc = lc.cpu().numpy().astype(np.float64)
+        latency["expansions_mean"] = float(lcc[:, 2].mean())
+        if "stamps" not in os.environ.get("NGT_AMD_LIB", ""):
+            latency["stalled_pops_mean"] = float(lcc[:, 3].mean())
+            log("single-query: %.0f expansions, %.0f of them waited for their list" % (
+                lcc[:, 2].mean(), lcc[:, 3].mean()))
+        else:
+            tot = lcc[:, [5, 6, 1, 7]].mean(0)
+            log("single-query phase cycles (latency kernel): pop %.3g wait %.3g list+accept %.3g feed %.3g "
+                "(sum %.3g); expansions %.0f, never handed out %.0f" % (
+                    tot[0], tot[1], tot[2], tot[3], tot.sum(), lcc[:, 2].mean(), lcc[:, 3].mean()))
 
     cpu = parity = None
     if rank == 0 and not args.no_cpu and world == 1 and not shard:

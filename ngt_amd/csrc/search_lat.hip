@@ -59,7 +59,8 @@ struct LatSlot {
 };
 
 struct LatLayout {
-  uint32_t off_slot, off_eid, off_ed, off_tail, off_res, off_q, off_qb, off_nid, off_nd, off_stg, off_bm, total;
+  uint32_t off_slot, off_eid, off_ed, off_tail, off_res, off_q, off_qb, off_nid, off_nd, off_hist, off_stg, off_bm,
+      total;
   __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
   __host__ __device__ LatLayout(const SearchArgs& a, uint32_t cap, uint32_t waves) {
     uint32_t o = up16(sizeof(LatCtl));
@@ -72,6 +73,7 @@ struct LatLayout {
     off_qb = o; o = up16(o + (uint32_t)a.dp);
     off_nid = o; o = up16(o + 256u);
     off_nd = o; o = up16(o + 256u);
+    off_hist = o; o = up16(o + 256u);
     off_stg = o; o = up16(o + 256u * waves);
     off_bm = o; o = up16(o + 4u * ((a.nrows + 31u) / 32u));
     total = o;
@@ -102,6 +104,57 @@ __device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// A threshold t over the keys of arr[0..n) that are <= lim (wave-uniform
+// arguments): at most M keys lie below t, at least one does, and M/2 or more
+// when the keys allow.  Histogram passes over 64 power-of-two bins of the key
+// range (64 LDS counters in hist), refining the first bin that overflows.
+// Returns 0 when no key is <= lim.  Not inlined: it runs a few times per
+// query and would otherwise share the commit loop's registers.
+__device__ __noinline__ uint64_t lat_select(const uint64_t* arr, uint32_t n, uint32_t M, uint64_t lim, uint32_t* hist) {
+  const int lane = lane_id();
+  uint64_t lo = ~0ull, hi = 0;
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint64_t v = arr[i];
+    if (v <= lim) {
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
+  }
+  lo = uniform_u64_lat(wave_min_u64(lo));
+  hi = uniform_u64_lat(~wave_min_u64(~hi));
+  if (lo > hi) return 0ull;
+  uint32_t base = 0;
+  for (int it = 0; it < 16; it++) {
+    const uint64_t span = hi - lo;
+    const int bits = span ? 64 - __clzll((long long)span) : 0;
+    const int shift = bits > 6 ? bits - 6 : 0;
+    // hist is LDS reached through a generic pointer: flat accesses may
+    // complete out of order, so each phase drains before the next
+    hist[lane] = 0u;
+    __threadfence_block();
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint64_t v = arr[i];
+      if (v >= lo && v <= hi && v <= lim) atomicAdd(hist + (uint32_t)((v - lo) >> shift), 1u);
+    }
+    __threadfence_block();
+    uint32_t incl = hist[lane];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    const uint32_t b = (uint32_t)__popcll(ballot64(base + incl <= M));  // bins [0, b) fit
+    if (b == 64u) return hi + 1;
+    const uint32_t below = base + (b ? (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)b - 1) : 0u);
+    if ((below >= M / 2 && below > 0) || shift == 0) return lo + ((uint64_t)b << shift);
+    base = below;
+    lo = lo + ((uint64_t)b << shift);
+    const uint64_t top = lo + ((1ull << shift) - 1ull);
+    hi = top < hi ? top : hi;
+  }
+  return lo + 1;  // never expected: the minimum alone
+}
+
 }  // namespace
 
 // NCH = dp / 16; W waves (1 commit + W-1 speculation); RG = 16-entry filter
@@ -125,6 +178,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
   uint32_t* nid = reinterpret_cast<uint32_t*>(smem + lay.off_nid);
   float* nd = reinterpret_cast<float*>(smem + lay.off_nd);
   uint32_t* bm = reinterpret_cast<uint32_t*>(smem + lay.off_bm);
+  // threshold-selection counters: not nid/nd, which hold the accept step's
+  // staged candidates when a full tail makes room in the middle of it
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lay.off_hist);
   uint32_t* stg = reinterpret_cast<uint32_t*>(smem + lay.off_stg) + 64 * (threadIdx.x >> 6);  // per wave
 
   const int lane = lane_id();
@@ -164,7 +220,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       double frq = 0.0;
       filter_query(qlds, a.dp, fa, fb, qb, fsq, frq);
       uint32_t nres = 0, maxq = 0;
-      uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0;
+      uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0;
+      // diagnostic build only: shader-clock totals per phase
+      uint64_t t_pop = 0, t_wait = 0, t_list = 0, t_feed = 0, t_last = 0;
+      (void)t_pop; (void)t_wait; (void)t_list; (void)t_feed; (void)t_last;
       float radius = a.radius;
       float expr = 0.f;
       // unchecked set: head (registers, sorted, hn keys) < B <= tail (LDS,
@@ -188,9 +247,12 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           nspill++;
         }
       };
+      auto select_t = [&](const uint64_t* arr, uint32_t n, uint32_t M, uint64_t lim) -> uint64_t {
+        return lat_select(arr, n, M, lim, hist);
+      };
       // the tail is full: drop keys beyond the exploration radius (never
       // popped, Graph.cpp:433-435); if still over half full, move the keys
-      // from the median up to the spill (T drops)
+      // from a threshold up to the spill (T drops)
       auto tail_room = [&]() {
         uint32_t out = 0;
         for (uint32_t b0 = 0; b0 < ntail; b0 += 64) {
@@ -206,27 +268,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         ntail = out;
         const uint32_t keep = a.lat_tail / 2;
         if (ntail <= keep) return;
-        uint64_t lo = ~0ull, hi = 0;
-        for (uint32_t i = lane; i < ntail; i += 64) {
-          const uint64_t v = tail[i];
-          lo = v < lo ? v : lo;
-          hi = v > hi ? v : hi;
-        }
-        lo = wave_min_u64(lo);
-        hi = ~wave_min_u64(~hi);
-        uint64_t l = lo, h = hi;
-        for (int it = 0; it < 64 && l < h; it++) {
-          const uint64_t mid = l + ((h - l) >> 1) + 1;
-          uint32_t c = 0;
-          for (uint32_t i = lane; i < ntail; i += 64) c += tail[i] < mid ? 1u : 0u;
-          c = wave_sum_u32(c);
-          if (c <= keep) {
-            l = mid;
-            if (c >= keep / 2) break;
-          } else {
-            h = mid - 1;
-          }
-        }
+        const uint64_t l = select_t(tail, ntail, keep, ~0ull);
         out = 0;
         for (uint32_t b0 = 0; b0 < ntail; b0 += 64) {
           const uint32_t i = b0 + (uint32_t)lane;
@@ -246,6 +288,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           __builtin_amdgcn_wave_barrier();
           out += (uint32_t)__popcll(km);
         }
+        if ((out == 0u || out > keep) && lane == 0) atomicOr(a.error, 32);  // selection check
         ntail = out;
         T = l;
       };
@@ -299,46 +342,19 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (q > maxq) maxq = q;
       };
       // an empty head takes the smallest keys of the tail (the tail the
-      // smallest of the spill first): bisection on the key for a threshold
-      // that moves 32..64 keys, then a bitonic sort across the lanes
+      // smallest of the spill first): a histogram threshold that moves 32..64
+      // keys, then a bitonic sort across the lanes
       auto refill_tail = [&]() {
-        // nothing in LDS: the smallest spill keys within the radius move in
+        // nothing in LDS: the smallest spill keys within the radius move in,
+        // the ones beyond it are dropped
         const uint32_t want = a.lat_tail / 2;
         const uint64_t lim = ((uint64_t)ord_of(expr) << 32) | 0xffffffffull;
-        uint64_t lo = ~0ull, hi = 0;
-        for (uint32_t i = lane; i < nspill; i += 64) {
-          const uint64_t v = spill[i];
-          if (v <= lim) {
-            lo = v < lo ? v : lo;
-            hi = v > hi ? v : hi;
-          }
-        }
-        lo = wave_min_u64(lo);
-        hi = ~wave_min_u64(~hi);
-        if (lo > hi) {  // nothing within the radius: the search ends
+        const uint64_t l = select_t(spill, nspill, want, lim);
+        if (l == 0ull) {  // nothing within the radius: the search ends
           nspill = 0;
           T = ~0ull;
           return;
         }
-        uint64_t l = lo, h = hi;  // largest t with count(lo <= keys < t) <= want
-        if (true) {
-          uint32_t c = 0;
-          for (uint32_t i = lane; i < nspill; i += 64) c += spill[i] <= hi ? 1u : 0u;
-          if (wave_sum_u32(c) <= want) l = hi + 1;  // everything within the radius fits
-        }
-        for (int it = 0; it < 64 && l < h; it++) {
-          const uint64_t mid = l + ((h - l) >> 1) + 1;
-          uint32_t c = 0;
-          for (uint32_t i = lane; i < nspill; i += 64) c += spill[i] < mid ? 1u : 0u;
-          c = wave_sum_u32(c);
-          if (c <= want) {
-            l = mid;
-            if (c >= want / 2) break;
-          } else {
-            h = mid - 1;
-          }
-        }
-        if (l == lo) l = lo + 1;  // at least the minimum moves
         uint32_t out = 0;
         for (uint32_t b0 = 0; b0 < nspill; b0 += 64) {
           const uint32_t i = b0 + (uint32_t)lane;
@@ -356,38 +372,13 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         nspill = out;
         T = nspill ? l : ~0ull;
+        if ((ntail == 0u || ntail > want) && lane == 0) atomicOr(a.error, 64);  // selection check
       };
       auto refill_head = [&]() {
         if (ntail == 0 && nspill != 0) refill_tail();
         if (ntail == 0) return;
-        // threshold t with 32 <= count(tail keys < t) <= 64 (or all of them)
-        uint64_t lo = ~0ull, hi = 0;
-        for (uint32_t i = lane; i < ntail; i += 64) {
-          const uint64_t v = tail[i];
-          lo = v < lo ? v : lo;
-          hi = v > hi ? v : hi;
-        }
-        lo = wave_min_u64(lo);
-        hi = ~wave_min_u64(~hi);
-        uint64_t t;
-        if (ntail <= 64u) {
-          t = hi + 1;  // all (hi < ~0: keys carry a finite ordinal)
-        } else {
-          uint64_t l = lo + 1, h = hi;
-          for (int it = 0; it < 64 && l < h; it++) {
-            const uint64_t mid = l + ((h - l) >> 1) + 1;
-            uint32_t c = 0;
-            for (uint32_t i = lane; i < ntail; i += 64) c += tail[i] < mid ? 1u : 0u;
-            c = wave_sum_u32(c);
-            if (c <= 64u) {
-              l = mid;
-              if (c >= 32u) break;
-            } else {
-              h = mid - 1;
-            }
-          }
-          t = l;
-        }
+        // the (at most 64, at least 32 when there are) smallest tail keys
+        const uint64_t t = select_t(tail, ntail, 64u, ~0ull);
         // move tail keys < t into the head lanes (unsorted), compact the tail
         uint64_t v = ~0ull;
         uint32_t got = 0, out = 0;
@@ -413,6 +404,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           v = (uint32_t)lane < got ? st64[lane] : ~0ull;
         }
         ntail = out;
+        if ((got == 0u || got > 64u) && lane == 0) atomicOr(a.error, 128);  // selection check
         // bitonic sort of the 64 lanes (ascending; empty lanes hold ~0)
 #pragma unroll
         for (int kk = 2; kk <= 64; kk <<= 1) {
@@ -558,6 +550,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       feed();
 
       // ---- best-first loop (Graph.cpp:430-486) ------------------------------
+#ifdef NGT_AMD_STAMPS
+      t_last = stamp();
+#endif
       for (;;) {
         uint64_t key;
         uint32_t tag;
@@ -568,7 +563,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           nwait++;
         }
         if (stuck) break;
+        NGT_MARK(t_pop);
         feed();  // keep the speculation ahead while this node's list lands
+        NGT_MARK(t_feed);
+        if (lds_load_acq(&slots[tag].state) != kReady) nstall++;
         for (uint32_t spin = 0; lds_load_acq(&slots[tag].state) != kReady; spin++) {
           if (spin > (1u << 24)) {
             if (lane == 0) atomicOr(a.error, 16);
@@ -578,6 +576,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           __builtin_amdgcn_s_sleep(1);
         }
         if (stuck) break;
+        NGT_MARK(t_wait);
         const uint32_t n = slots[tag].n;
         nexp++;
         nedge += slots[tag].deg;
@@ -606,7 +605,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         if (lane == 0) slots[tag].state = kFree;
         freem |= 1ull << tag;
+        NGT_MARK(t_list);
         feed();
+        NGT_MARK(t_feed);
       }
       // the speculation waves leave once every issued slot is done
       __builtin_amdgcn_wave_barrier();
@@ -624,11 +625,20 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           c[0] = ndist;
           c[1] = ndist - ns;
           c[2] = nexp;
-          c[3] = nwait;  // pops whose list nobody had evaluated yet
+          c[3] = nstall;  // pops that waited for their list (nwait of them: not yet handed out)
           c[4] = nedge;
           c[5] = maxq;
           c[6] = nexact;
           c[7] = ns;
+#ifdef NGT_AMD_STAMPS
+          // phase cycles: [5] pop (+ refills, issue), [6] wait for the list,
+          // [1] list + accept, [7] feeding the speculation; [3] nwait
+          c[5] = t_pop;
+          c[6] = t_wait;
+          c[1] = t_list;
+          c[7] = t_feed;
+          c[3] = nwait;
+#endif
         }
       }
     } else {
@@ -779,9 +789,9 @@ hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStrea
     hipLaunchKernelGGL(kern, dim3(slots), dim3(512), lds, s, a);                                                \
   } while (0)
   if (a.dp == 128) {
-    if (cap <= 64) LAT(8, 4); else LAT(8, 10);
+    if (cap <= 64) LAT(8, 4); else LAT(8, 8);
   } else {
-    if (cap <= 64) LAT(6, 4); else LAT(6, 10);
+    if (cap <= 64) LAT(6, 4); else LAT(6, 8);
   }
 #undef LAT
   return hipGetLastError();

@@ -7,7 +7,8 @@ mkdir -p "profiles/$dst"
 for f in gpurun_out/$src/*; do
   b=$(basename "$f")
   case "$b" in
-    *_kernel_trace.csv|*_kernel_stats.csv) { head -1 "$f"; grep "ngt_amd" "$f"; } > "profiles/$dst/$b" ;;
+    *_kernel_stats.csv) { head -1 "$f"; grep "ngt_amd" "$f"; } > "profiles/$dst/$b" ;;
+    *_kernel_trace.csv) { head -1 "$f"; grep -E "search_(la_|lat_)?kernel|qg_search_kernel|scan_mfma_kernel" "$f"; } > "profiles/$dst/$b" ;;
     *.json|*.log) cp "$f" "profiles/$dst/$b" ;;
   esac
 done
