@@ -118,6 +118,7 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
   HIP_OK(ix->adj.alloc((size_t)ix->nrows * b->adj_stride));
   HIP_OK(hipMemset(ix->adj.p, 0, (size_t)ix->nrows * b->adj_stride * sizeof(uint32_t)));
   ix->adj_stride = b->adj_stride;
+  ix->adj_version++;
   // the construction's searches read at most adj_stride edges of a list: the
   // padded copy is always the one to use (run_search never rebuilds it here)
   ix->max_degree = b->adj_stride;
@@ -131,6 +132,13 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
 extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64_t end_id) {
   if (!ix || !ix->build) return fail("ngt_amd_build_insert: call ngt_amd_build_begin first");
   HIP_OK(hipSetDevice(ix->device));
+  // the insertion searches must not build copies derived from the adjacency
+  // this call keeps changing (ensure_ncodes)
+  struct Building {
+    ngt_amd_index* ix;
+    ~Building() { ix->building = false; }
+  } building_guard{ix};
+  ix->building = true;
   BuildState& b = *ix->build;
   hipStream_t s = ix->stream;
   const uint64_t rb = ix->row_bytes;
@@ -391,6 +399,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
     HIP_OK(d_dirty.upload(dirty.data(), dirty.size()));
     HIP_OK(d_vals.upload(vals.data(), vals.size()));
     HIP_OK(launch_adj_scatter(ix->adj.p, b.adj_stride, d_dirty.p, d_vals.p, (uint32_t)dirty.size(), s));
+    ix->adj_version++;
     uint32_t hc[3];
     int herr = 0;
     HIP_OK(hipMemcpyAsync(hc, b.counts.p, sizeof hc, hipMemcpyDeviceToHost, s));
@@ -447,6 +456,7 @@ extern "C" int ngt_amd_build_set_graph(ngt_amd_index* ix, const uint64_t* offset
     if (e1 > e0) b.graph_size = v + 1;
   }
   HIP_OK(hipMemcpy(ix->adj.p, adj.data(), adj.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  ix->adj_version++;
   return 0;
 }
 

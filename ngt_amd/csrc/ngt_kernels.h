@@ -95,6 +95,9 @@ struct SearchArgs {
   // latency kernel (search_lat.hip): speculation slots and LDS tail keys
   uint32_t lat_slots;
   uint32_t lat_tail;
+  // adjacency-ordered copy of the filter codes [nrows][adj_stride][fstride]
+  // (entry j of node v = the codes of adj[v][j]), or null
+  const uint8_t* ncodes;
 };
 
 // lookahead targets per step of search_la.hip: mode 0 (throughput, one wave
@@ -436,6 +439,8 @@ struct IvfSearchArgs {
 size_t ivf_search_lds_bytes(const IvfSearchArgs& a);
 // 1-byte filter copy of an L2 float repository: codes [nrows][dp], st [5]
 // scratch, params [5] = {a, b, E, X, valid}
+hipError_t launch_ncodes_build(const uint32_t* adj, uint64_t adj_stride, uint64_t nrows, const uint8_t* codes,
+                              uint64_t fstride, uint8_t* out, hipStream_t s);
 hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint64_t stride,
                                uint8_t* codes,
                                uint32_t* st, float* params, hipStream_t s);

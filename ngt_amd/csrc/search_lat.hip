@@ -46,6 +46,7 @@ struct LatCtl {
   uint32_t qi;
   uint32_t fthr;  // filter threshold of the current exploration radius
   uint32_t fsq;   // sum q''^2
+  uint64_t sp[4]; // diagnostic build: speculation-wave cycles (adjacency, filter, exact, idle)
 };
 
 // one node's speculation: key (its unchecked-set key, the priority), state,
@@ -84,6 +85,22 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
   const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
   return ((uint64_t)hi << 32) | lo;
+}
+// whole-wave lane shifts by one on the DPP path (gfx9 wave_shr:1 /
+// wave_shl:1: one VALU op instead of an LDS-crossbar ds_bpermute): up1 gives
+// lane i the value of lane i-1, down1 the value of lane i+1; the lane with
+// no source keeps its own value (the callers overwrite or mask it)
+__device__ __forceinline__ uint32_t wave_up1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_down1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint64_t wave_up1_u64(uint64_t v) {
+  return ((uint64_t)wave_up1((uint32_t)(v >> 32)) << 32) | wave_up1((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t wave_down1_u64(uint64_t v) {
+  return ((uint64_t)wave_down1((uint32_t)(v >> 32)) << 32) | wave_down1((uint32_t)v);
 }
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
@@ -210,7 +227,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       uint4* d = reinterpret_cast<uint4*>(qlds);
       for (uint32_t i = tid; i < (uint32_t)a.dp / 4; i += NT) d[i] = s[i];
       for (uint32_t i = tid; i < nslots; i += NT) slots[i].state = kFree;
-      if (tid == 0) ctl->done = 0u;
+      if (tid == 0) {
+        ctl->done = 0u;
+        ctl->sp[0] = ctl->sp[1] = ctl->sp[2] = ctl->sp[3] = 0ull;
+      }
     }
     __syncthreads();
 
@@ -322,15 +342,15 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
             }
             const uint64_t e = readlane_u64(hk, 63);
             orphan_tag((uint32_t)__builtin_amdgcn_readlane((int)ht, 63));
-            const uint64_t uk = shfl_u64(hk, lane > 0 ? lane - 1 : 0);
-            const uint32_t ut = (uint32_t)__shfl((int)ht, lane > 0 ? lane - 1 : 0, 64);
+            const uint64_t uk = wave_up1_u64(hk);
+            const uint32_t ut = wave_up1(ht);
             if ((uint32_t)lane > pos) { hk = uk; ht = ut; }
             if ((uint32_t)lane == pos) { hk = key; ht = kNoTag; }
             B = e;
             tail_push(e);
           } else {
-            const uint64_t uk = shfl_u64(hk, lane > 0 ? lane - 1 : 0);
-            const uint32_t ut = (uint32_t)__shfl((int)ht, lane > 0 ? lane - 1 : 0, 64);
+            const uint64_t uk = wave_up1_u64(hk);
+            const uint32_t ut = wave_up1(ht);
             if ((uint32_t)lane > pos && (uint32_t)lane <= hn) { hk = uk; ht = ut; }
             if ((uint32_t)lane == pos) { hk = key; ht = kNoTag; }
             hn++;
@@ -427,8 +447,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (hn == 0) return false;
         key = readlane_u64(hk, 0);
         tag = (uint32_t)__builtin_amdgcn_readlane((int)ht, 0);
-        const uint64_t dk = shfl_u64(hk, lane < 63 ? lane + 1 : 63);
-        const uint32_t dt = (uint32_t)__shfl((int)ht, lane < 63 ? lane + 1 : 63, 64);
+        const uint64_t dk = wave_down1_u64(hk);
+        const uint32_t dt = wave_down1(ht);
         hk = (uint32_t)lane < hn - 1 ? dk : ~0ull;
         ht = (uint32_t)lane < hn - 1 ? dt : kNoTag;
         hn--;
@@ -519,6 +539,42 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
       };
 
+      // the same accept on candidates held in registers: lanes of `cmask`
+      // (neighbour order = lane order), ids in idv, distances in dv -- no LDS
+      // staging on the commit path
+      auto accept_reg = [&](uint64_t cmask, uint32_t idv, float dv) {
+        auto push = [&](uint64_t m) {
+          while (m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            insert_key(make_key(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), j)),
+                                (uint32_t)__builtin_amdgcn_readlane((int)idv, j)));
+          }
+        };
+        uint64_t okmask = cmask & ballot64(dv <= expr);
+        while (okmask) {
+          const uint64_t rmask = okmask & ballot64(dv <= radius);
+          if (rmask == 0ull) {
+            push(okmask);
+            break;
+          }
+          const int j = __ffsll((long long)rmask) - 1;
+          push(okmask & ((1ull << j) - 1ull));
+          const uint64_t key = make_key(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), j)),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)idv, j));
+          insert_key(key);
+          res_insert(res, nres, k, key);
+          if (nres >= k) {
+            radius = key_dist(res[k - 1]);
+            expr = __fmul_rn(a.coef, radius);
+            set_fthr();
+          }
+          __builtin_amdgcn_wave_barrier();
+          okmask &= ~((2ull << j) - 1ull);
+          okmask &= ballot64(dv <= expr);
+        }
+      };
+
       // ---- setupDistances + setupSeeds (Graph.cpp:293-367) ----------------
       const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
       ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
@@ -582,26 +638,34 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         nedge += slots[tag].deg;
         const uint32_t* sid = eid + tag * cap;
         const float* sd = ed + tag * cap;
-        for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-          const uint32_t e = e0 + (uint32_t)lane;
-          const uint32_t id = e < n ? sid[e] : 0u;
-          const float d = e < n ? sd[e] : 0.f;
-          // ids of one list are distinct: test and mark in parallel
-          const bool fresh = e < n && !bm_test(bm, id);
-          if (fresh) atomicOr(bm + (id >> 5), 1u << (id & 31));
-          ndist += (uint32_t)__popcll(ballot64(fresh));
-          const bool keep = fresh && d <= expr;  // d = +inf: rejected by the bound
-          const uint64_t km = ballot64(keep);
-          nexact += (uint32_t)__popcll(ballot64(fresh && d != __builtin_huge_valf()));
-          __builtin_amdgcn_wave_barrier();
-          if (keep) {
-            nid[mbcnt(km)] = id;
-            nd[mbcnt(km)] = d;
+        // the whole list (<= 256 entries: 4 per lane) in one pass -- every
+        // load issued before the first visited test, every test before the
+        // marks -- then the accepts in neighbour order.  Ids of one list are
+        // distinct, so testing and marking them in parallel is the sequential
+        // outcome.
+        {
+          uint32_t id4[4];
+          float d4[4];
+          bool f4[4];
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            const uint32_t e = 64u * c + (uint32_t)lane;
+            id4[c] = e < n ? sid[e] : 0u;
+            d4[c] = e < n ? sd[e] : 0.f;
           }
-          __builtin_amdgcn_wave_barrier();
-          const uint32_t me = (uint32_t)__popcll(km);
-          if (me) accept(me);
-          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int c = 0; c < 4; c++) f4[c] = id4[c] != 0u && !bm_test(bm, id4[c]);
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            if (64u * c >= n) break;
+            if (f4[c]) atomicOr(bm + (id4[c] >> 5), 1u << (id4[c] & 31));
+            ndist += (uint32_t)__popcll(ballot64(f4[c]));
+            nexact += (uint32_t)__popcll(ballot64(f4[c] && d4[c] != __builtin_huge_valf()));
+            // candidates within the radius (d = +inf: rejected by the bound),
+            // accepted in neighbour order against the shrinking radius
+            const uint64_t km = ballot64(f4[c] && d4[c] <= expr);
+            if (km) accept_reg(km, id4[c], d4[c]);
+          }
         }
         if (lane == 0) slots[tag].state = kFree;
         freem |= 1ull << tag;
@@ -638,6 +702,12 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           c[1] = t_list;
           c[7] = t_feed;
           c[3] = nwait;
+          // speculation waves, summed over the waves: [0] adjacency + visited
+          // pre-test, [4] filter codes, [2] exact rows (expansions: nexp)
+          __builtin_amdgcn_s_waitcnt(0);
+          c[0] = ctl->sp[0];
+          c[4] = ctl->sp[1];
+          c[2] = ctl->sp[2];
 #endif
         }
       }
@@ -659,15 +729,79 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (lane == 0) old = atomicCAS(&slots[s].state, kIssued, kTaken);
         if ((uint32_t)__builtin_amdgcn_readfirstlane((int)old) != kIssued) continue;  // another wave took it
         const uint32_t node = key_id(m);
-        // adjacency row: the first min(degree, edgeSize) ids (Graph.cpp:436-439)
-        uint32_t r0, r1, r2, r3;
-        load_adj_row(a.adj + (uint64_t)node * a.adj_stride, cap, r0, r1, r2, r3);
-        const uint32_t deg = (uint32_t)(__popcll(ballot64(r0 != 0u)) + __popcll(ballot64(r1 != 0u)) +
-                                        __popcll(ballot64(r2 != 0u)) + __popcll(ballot64(r3 != 0u)));
-        // neighbours not visited yet, compacted in list order
+#ifdef NGT_AMD_STAMPS
+        uint64_t st0 = stamp();
+#endif
         uint32_t* sid = eid + s * cap;
         float* sd = ed + s * cap;
-        uint32_t n = 0;
+        uint32_t n = 0, deg = 0;
+        // the filter threshold of the current exploration radius (it only
+        // shrinks: a neighbour the bound rejects is outside the radius at
+        // commit time too)
+        const uint32_t fthr = lds_load_acq(&ctl->fthr), fsq = ctl->fsq;
+        uint2 q[NW];
+        {
+          const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
+#pragma unroll
+          for (int w = 0; w < NW; w++) q[w] = qp[w];
+        }
+        if (a.ncodes) {
+          // adjacency-ordered filter codes: the ids of a list and their codes
+          // arrive in ONE round trip (16 entries per RG group, a quad per
+          // entry); fresh entries (not visited when read) are compacted in
+          // list order with their bound verdict
+          constexpr int RGN = RG < 6 ? RG : 6;  // 96 entries in flight (VGPR budget)
+          const uint32_t* arow = a.adj + (uint64_t)node * a.adj_stride;
+          const uint8_t* nc = a.ncodes + (uint64_t)node * a.adj_stride * (4 * E);
+          for (uint32_t base = 0; base < cap; base += 16u * RGN) {
+            uint32_t ids[RGN];
+            uint2 c[RGN][NW];
+#pragma unroll
+            for (int j = 0; j < RGN; j++) {
+              const uint32_t e = base + 16u * j + (uint32_t)rs;
+              ids[j] = 0u;
+              if (base + 16u * j < cap) {
+                ids[j] = e < cap ? arow[e] : 0u;
+                const uint2* cp = reinterpret_cast<const uint2*>(nc + (uint64_t)(e < cap ? e : 0u) * (4 * E)) + g * NW;
+#pragma unroll
+                for (int w = 0; w < NW; w++) c[j][w] = cp[w];
+              }
+            }
+            bool ended = false;
+#pragma unroll
+            for (int j = 0; j < RGN; j++) {
+              if (base + 16u * j >= cap || ended) continue;
+              const uint32_t id = ids[j];
+              uint32_t qc = 0u, cc = 0u;
+#pragma unroll
+              for (int w = 0; w < NW; w++) {
+                qc = __builtin_amdgcn_udot4(q[w].x, c[j][w].x, qc, false);
+                qc = __builtin_amdgcn_udot4(q[w].y, c[j][w].y, qc, false);
+                cc = __builtin_amdgcn_udot4(c[j][w].x, c[j][w].x, cc, false);
+                cc = __builtin_amdgcn_udot4(c[j][w].y, c[j][w].y, cc, false);
+              }
+              const uint32_t S = fsq + quad_sum_u32(cc - 2u * qc);
+              const bool fresh = g == 0 && id != 0u && !bm_test(bm, id);
+              const uint64_t fm = ballot64(fresh);
+              if (fresh) {
+                sid[n + mbcnt(fm)] = id;
+                // survivors: -1 until their exact distance lands; the rest +inf
+                sd[n + mbcnt(fm)] = S <= fthr ? -1.f : __builtin_huge_valf();
+              }
+              n += (uint32_t)__popcll(fm);
+              const uint32_t live = (uint32_t)__popcll(ballot64(g == 0 && id != 0u));
+              deg += live;
+              ended = live < 16u;  // 0-terminated rows: the list ends in this group
+            }
+            if (ended) break;
+          }
+          __builtin_amdgcn_wave_barrier();
+        } else {
+        // adjacency row: the first min(degree, edgeSize) ids (Graph.cpp:436-439)
+        uint32_t r0, r1, r2, r3;
+        load_adj_row(a.adj + (uint64_t)node * a.adj_stride, cap, r0, r1, r2, r3);        deg = (uint32_t)(__popcll(ballot64(r0 != 0u)) + __popcll(ballot64(r1 != 0u)) +
+                                        __popcll(ballot64(r2 != 0u)) + __popcll(ballot64(r3 != 0u)));
+        // neighbours not visited yet, compacted in list order
         {
           const uint32_t rr[4] = {r0, r1, r2, r3};
 #pragma unroll
@@ -680,14 +814,16 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           }
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef NGT_AMD_STAMPS
+        {
+          const uint64_t t1 = stamp();
+          if (lane == 0) atomicAdd((unsigned long long*)&ctl->sp[0], (unsigned long long)(t1 - st0));
+          st0 = t1;
+        }
+#endif
         // filter codes of every entry (quad per entry), RG groups of 16 in
         // flight; the threshold of the current exploration radius (it only
         // shrinks: a rejected neighbour is outside the radius at commit too)
-        const uint32_t fthr = lds_load_acq(&ctl->fthr), fsq = ctl->fsq;
-        uint2 q[NW];
-        const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
-#pragma unroll
-        for (int w = 0; w < NW; w++) q[w] = qp[w];
         for (uint32_t base = 0; base < n; base += 16u * RG) {
           uint2 c[RG][NW];
 #pragma unroll
@@ -717,7 +853,15 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
             if (g == 0 && e < n) sd[e] = S <= fthr ? -1.f : __builtin_huge_valf();
           }
         }
+        }  // the gathered-codes path
         __builtin_amdgcn_wave_barrier();
+#ifdef NGT_AMD_STAMPS
+        {
+          const uint64_t t1 = stamp();
+          if (lane == 0) atomicAdd((unsigned long long*)&ctl->sp[1], (unsigned long long)(t1 - st0));
+          st0 = t1;
+        }
+#endif
         // exact comparator distances of the survivors (PrimitiveComparator::
         // compareL2 through l2_fold_rows), 16 rows per wave step
         {
@@ -755,6 +899,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           }
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef NGT_AMD_STAMPS
+        if (lane == 0) atomicAdd((unsigned long long*)&ctl->sp[2], (unsigned long long)(stamp() - st0));
+#endif
         if (lane == 0) {
           slots[s].n = n;
           slots[s].deg = deg;
@@ -789,9 +936,9 @@ hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStrea
     hipLaunchKernelGGL(kern, dim3(slots), dim3(512), lds, s, a);                                                \
   } while (0)
   if (a.dp == 128) {
-    if (cap <= 64) LAT(8, 4); else LAT(8, 8);
+    if (cap <= 64) LAT(8, 4); else LAT(8, 5);
   } else {
-    if (cap <= 64) LAT(6, 4); else LAT(6, 8);
+    if (cap <= 64) LAT(6, 4); else LAT(6, 6);
   }
 #undef LAT
   return hipGetLastError();
