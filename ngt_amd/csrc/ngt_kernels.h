@@ -104,8 +104,8 @@ struct SearchArgs {
 // per query), mode 1 (latency, eight waves per query)
 inline uint32_t la_targets(int mode) {
   if (mode != 0) return 8u;
-  const char* v = getenv("NGT_AMD_LA_P");  // 3 (default: fewer discarded targets per step) or 4
-  return v && atoi(v) == 4 ? 4u : 3u;
+  const char* v = getenv("NGT_AMD_LA_P");  // 3 (default), 2 (fewer discarded targets) or 4
+  return v && atoi(v) == 4 ? 4u : (v && atoi(v) == 2 ? 2u : 3u);
 }
 // resident waves per SIMD of the throughput form: 4 (128 VGPRs, 4 filter
 // groups in flight, 256 LDS keys, 16 Kbit filter: <= 10 KB of LDS so 16

@@ -887,6 +887,8 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
   if (mode == 0) {
     if (P == 3) {
       if (a.dp == 128) LA_T(8, 3); else LA_T(6, 3);
+    } else if (P == 2) {
+      if (a.dp == 128) LA_T(8, 2); else LA_T(6, 2);
     } else {
       if (a.dp == 128) LA_T(8, 4); else LA_T(6, 4);
     }
