@@ -133,7 +133,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   if (!ix || !ix->build) return fail("ngt_amd_build_insert: call ngt_amd_build_begin first");
   HIP_OK(hipSetDevice(ix->device));
   // the insertion searches must not build copies derived from the adjacency
-  // this call keeps changing (ensure_ncodes)
+  // this call keeps changing
   struct Building {
     ngt_amd_index* ix;
     ~Building() { ix->building = false; }

@@ -109,30 +109,6 @@ __global__ void ngt_filter_finalize_kernel(const uint32_t* st, float* params) {
   params[4] = st[2] ? 0.0f : 1.0f;
 }
 
-// Adjacency-ordered copy of the filter codes: entry j of node v holds the
-// code row of adj[v][j] (zeros where the padded row ends), so a search reads
-// a list's ids and its neighbours' codes together, in one round trip, as
-// contiguous bytes instead of a gather.  16 B per thread, grid-stride.
-__global__ void __launch_bounds__(256) ngt_ncodes_build_kernel(const uint32_t* adj, uint64_t adj_stride, uint64_t nrows,
-                                                               const uint8_t* codes, uint64_t fstride, uint8_t* out) {
-  const uint64_t per = fstride / 16;  // 16-byte pieces per code row
-  const uint64_t total = nrows * adj_stride * per;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t entry = t / per, piece = t - entry * per;
-    const uint32_t id = adj[entry];
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (id != 0u) v = reinterpret_cast<const uint4*>(codes + (uint64_t)id * fstride)[piece];
-    reinterpret_cast<uint4*>(out + entry * fstride)[piece] = v;
-  }
-}
-
-hipError_t launch_ncodes_build(const uint32_t* adj, uint64_t adj_stride, uint64_t nrows, const uint8_t* codes,
-                              uint64_t fstride, uint8_t* out, hipStream_t s) {
-  if (fstride % 16 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ngt_ncodes_build_kernel, dim3(8192), dim3(256), 0, s, adj, adj_stride, nrows, codes, fstride, out);
-  return hipGetLastError();
-}
-
 hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint64_t stride,
                                uint8_t* codes, uint32_t* st, float* params, hipStream_t s) {
   hipError_t e = hipMemsetAsync(st, 0xff, sizeof(uint32_t), s);

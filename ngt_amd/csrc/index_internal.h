@@ -216,10 +216,7 @@ struct ngt_amd_index {
   uint64_t max_degree = 0;       // widest adjacency list
   uint64_t adj_version = 0;      // bumped whenever adj changes
   bool building = false;         // ANNG construction in progress (adj changes per batch)
-  struct {                       // adjacency-ordered filter codes [nrows][adj_stride][filt.stride]
-    DevBuf<uint8_t> codes;
-    uint64_t adj_version = ~0ull, rows_version = ~0ull, adj_stride = 0;
-  } ncodes;
+
   bool has_graph = false;
   std::vector<uint8_t> h_graph_empty;
   // tree

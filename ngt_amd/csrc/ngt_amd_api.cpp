@@ -159,39 +159,6 @@ static int build_padded_adjacency(ngt_amd_index* ix, uint64_t need) {
   return 0;
 }
 
-// The adjacency-ordered filter codes (filter_kernels.hip: ngt_ncodes_build_kernel)
-// for the latency kernel's speculation: built once per version of the rows
-// and of the padded adjacency, never during construction (the adjacency
-// changes every batch there), and only when they take at most a quarter of
-// the free HBM (C2: 1M x 160 x 128 B = 20.5 GB).  Caller holds ix->mu.
-static const uint8_t* ensure_ncodes(ngt_amd_index* ix) {
-  // opt-in: on C2 single queries it measured 2.94 ms against 2.74 ms without
-  // it (profiles/r3/lat2): the speculation is not bound by the gather
-  static const bool on = [] {
-    const char* v = getenv("NGT_AMD_NCODES");
-    return v && atoi(v) != 0;
-  }();
-  if (!on || ix->building || !ix->adj.p || ix->filt.version != ix->rows_version || ix->filt.stride % 16) return nullptr;
-  auto& n = ix->ncodes;
-  if (n.codes.p && n.adj_version == ix->adj_version && n.rows_version == ix->rows_version && n.adj_stride == ix->adj_stride)
-    return n.codes.p;
-  n.codes.release();
-  const uint64_t bytes = ix->nrows * ix->adj_stride * ix->filt.stride;
-  size_t freeb = 0, totalb = 0;
-  if (hipMemGetInfo(&freeb, &totalb) != hipSuccess || (double)bytes > 0.25 * (double)freeb) return nullptr;
-  if (n.codes.alloc(bytes) != hipSuccess) return nullptr;
-  if (launch_ncodes_build(ix->adj.p, ix->adj_stride, ix->nrows, ix->filt.codes.p, ix->filt.stride, n.codes.p,
-                          ix->stream) != hipSuccess ||
-      hipStreamSynchronize(ix->stream) != hipSuccess) {
-    n.codes.release();
-    return nullptr;
-  }
-  n.adj_version = ix->adj_version;
-  n.rows_version = ix->rows_version;
-  n.adj_stride = ix->adj_stride;
-  return n.codes.p;
-}
-
 static uint64_t max_degree_of(const uint64_t* h_offsets, uint64_t nrows) {
   uint64_t maxdeg = 0;
   for (uint64_t i = 0; i < nrows; i++) maxdeg = std::max<uint64_t>(maxdeg, h_offsets[i + 1] - h_offsets[i]);
@@ -673,8 +640,6 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       if (search_lat_lds_bytes(b) <= lds_max) {
         a = b;
         lat = true;
-        std::lock_guard<std::mutex> lk(ix->mu);
-        a.ncodes = ensure_ncodes(ix);
       }
     }
   }

@@ -95,17 +95,17 @@ struct SearchArgs {
   // latency kernel (search_lat.hip): speculation slots and LDS tail keys
   uint32_t lat_slots;
   uint32_t lat_tail;
-  // adjacency-ordered copy of the filter codes [nrows][adj_stride][fstride]
-  // (entry j of node v = the codes of adj[v][j]), or null
-  const uint8_t* ncodes;
 };
 
 // lookahead targets per step of search_la.hip: mode 0 (throughput, one wave
 // per query), mode 1 (latency, eight waves per query)
 inline uint32_t la_targets(int mode) {
   if (mode != 0) return 8u;
-  const char* v = getenv("NGT_AMD_LA_P");  // 3 (default), 2 (fewer discarded targets) or 4
-  return v && atoi(v) == 4 ? 4u : (v && atoi(v) == 2 ? 2u : 3u);
+  // 2 (default: ANNG 88.4k QPS vs 72.5k at 3 and 57.8k at 4 targets per
+  // step, profiles/r3/anng_p), or NGT_AMD_LA_P = 1 / 3 / 4
+  const char* v = getenv("NGT_AMD_LA_P");
+  const int p = v ? atoi(v) : 2;
+  return p == 1 ? 1u : (p == 3 ? 3u : (p == 4 ? 4u : 2u));
 }
 // resident waves per SIMD of the throughput form: 4 (128 VGPRs, 4 filter
 // groups in flight, 256 LDS keys, 16 Kbit filter: <= 10 KB of LDS so 16
@@ -439,8 +439,6 @@ struct IvfSearchArgs {
 size_t ivf_search_lds_bytes(const IvfSearchArgs& a);
 // 1-byte filter copy of an L2 float repository: codes [nrows][dp], st [5]
 // scratch, params [5] = {a, b, E, X, valid}
-hipError_t launch_ncodes_build(const uint32_t* adj, uint64_t adj_stride, uint64_t nrows, const uint8_t* codes,
-                              uint64_t fstride, uint8_t* out, hipStream_t s);
 hipError_t launch_filter_build(const uint8_t* rows, uint64_t row_bytes, uint64_t nrows, uint32_t dp, uint64_t stride,
                                uint8_t* codes,
                                uint32_t* st, float* params, hipStream_t s);

@@ -889,6 +889,8 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
       if (a.dp == 128) LA_T(8, 3); else LA_T(6, 3);
     } else if (P == 2) {
       if (a.dp == 128) LA_T(8, 2); else LA_T(6, 2);
+    } else if (P == 1) {
+      if (a.dp == 128) LA_T(8, 1); else LA_T(6, 1);
     } else {
       if (a.dp == 128) LA_T(8, 4); else LA_T(6, 4);
     }

@@ -745,58 +745,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
 #pragma unroll
           for (int w = 0; w < NW; w++) q[w] = qp[w];
         }
-        if (a.ncodes) {
-          // adjacency-ordered filter codes: the ids of a list and their codes
-          // arrive in ONE round trip (16 entries per RG group, a quad per
-          // entry); fresh entries (not visited when read) are compacted in
-          // list order with their bound verdict
-          constexpr int RGN = RG < 6 ? RG : 6;  // 96 entries in flight (VGPR budget)
-          const uint32_t* arow = a.adj + (uint64_t)node * a.adj_stride;
-          const uint8_t* nc = a.ncodes + (uint64_t)node * a.adj_stride * (4 * E);
-          for (uint32_t base = 0; base < cap; base += 16u * RGN) {
-            uint32_t ids[RGN];
-            uint2 c[RGN][NW];
-#pragma unroll
-            for (int j = 0; j < RGN; j++) {
-              const uint32_t e = base + 16u * j + (uint32_t)rs;
-              ids[j] = 0u;
-              if (base + 16u * j < cap) {
-                ids[j] = e < cap ? arow[e] : 0u;
-                const uint2* cp = reinterpret_cast<const uint2*>(nc + (uint64_t)(e < cap ? e : 0u) * (4 * E)) + g * NW;
-#pragma unroll
-                for (int w = 0; w < NW; w++) c[j][w] = cp[w];
-              }
-            }
-            bool ended = false;
-#pragma unroll
-            for (int j = 0; j < RGN; j++) {
-              if (base + 16u * j >= cap || ended) continue;
-              const uint32_t id = ids[j];
-              uint32_t qc = 0u, cc = 0u;
-#pragma unroll
-              for (int w = 0; w < NW; w++) {
-                qc = __builtin_amdgcn_udot4(q[w].x, c[j][w].x, qc, false);
-                qc = __builtin_amdgcn_udot4(q[w].y, c[j][w].y, qc, false);
-                cc = __builtin_amdgcn_udot4(c[j][w].x, c[j][w].x, cc, false);
-                cc = __builtin_amdgcn_udot4(c[j][w].y, c[j][w].y, cc, false);
-              }
-              const uint32_t S = fsq + quad_sum_u32(cc - 2u * qc);
-              const bool fresh = g == 0 && id != 0u && !bm_test(bm, id);
-              const uint64_t fm = ballot64(fresh);
-              if (fresh) {
-                sid[n + mbcnt(fm)] = id;
-                // survivors: -1 until their exact distance lands; the rest +inf
-                sd[n + mbcnt(fm)] = S <= fthr ? -1.f : __builtin_huge_valf();
-              }
-              n += (uint32_t)__popcll(fm);
-              const uint32_t live = (uint32_t)__popcll(ballot64(g == 0 && id != 0u));
-              deg += live;
-              ended = live < 16u;  // 0-terminated rows: the list ends in this group
-            }
-            if (ended) break;
-          }
-          __builtin_amdgcn_wave_barrier();
-        } else {
+        {
         // adjacency row: the first min(degree, edgeSize) ids (Graph.cpp:436-439)
         uint32_t r0, r1, r2, r3;
         load_adj_row(a.adj + (uint64_t)node * a.adj_stride, cap, r0, r1, r2, r3);        deg = (uint32_t)(__popcll(ballot64(r0 != 0u)) + __popcll(ballot64(r1 != 0u)) +
@@ -853,7 +802,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
             if (g == 0 && e < n) sd[e] = S <= fthr ? -1.f : __builtin_huge_valf();
           }
         }
-        }  // the gathered-codes path
+        }
         __builtin_amdgcn_wave_barrier();
 #ifdef NGT_AMD_STAMPS
         {
@@ -936,9 +885,9 @@ hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStrea
     hipLaunchKernelGGL(kern, dim3(slots), dim3(512), lds, s, a);                                                \
   } while (0)
   if (a.dp == 128) {
-    if (cap <= 64) LAT(8, 4); else LAT(8, 5);
+    if (cap <= 64) LAT(8, 4); else LAT(8, 9);
   } else {
-    if (cap <= 64) LAT(6, 4); else LAT(6, 6);
+    if (cap <= 64) LAT(6, 4); else LAT(6, 10);
   }
 #undef LAT
   return hipGetLastError();
