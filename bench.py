@@ -1320,6 +1320,8 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
         if r.returncode != 0:
             raise SystemExit("bench: capi_threads failed: %s" % r.stderr[-2000:])
         res = json.loads(r.stdout.strip().splitlines()[-1])
+        for ln in [x for x in r.stderr.splitlines() if x.startswith("[serve]")][:20]:
+            log("C client %d threads: %s" % (t, ln))
         ids = np.fromfile(ids_path, np.uint32).reshape(-1, K).astype(np.int64)
         qi = np.arange(ids.shape[0]) % Q.shape[0]
         res["recall_at_10"] = recall_at(ids, gt[qi], K)

@@ -159,6 +159,23 @@ int ngt_amd_tree_seeds_device(ngt_amd_index *index, const void *d_queries, uint6
  * one-expansion-per-pop kernel, 0 the lookahead kernel with a wave per query,
  * 1 the lookahead kernel with eight waves per query (search_la.hip). */
 int ngt_amd_last_search_lookahead(const ngt_amd_index *index);
+/* One query through the resident serving grid: the single-query search of
+ * ngt_search_index (lib/NGT/Capi.cpp:377-406 -> NeighborhoodGraph::search)
+ * for concurrent callers.  A long-lived launch of the latency kernel takes
+ * queries from a ring in pinned host memory as they are posted and answers
+ * each one as soon as it finishes (no launch per call, no batch waiting for
+ * its slowest member); it leaves by itself when idle.  query: host floats of
+ * the index's object dimension (L2 float rows of 96/128 padded elements);
+ * params->seed_mode NGT_AMD_SEED_RANDOM or NGT_AMD_SEED_TREE, k <= 64.
+ * Results, distances and counters equal ngt_amd_search's.  Thread-safe.
+ * Returns 0 when served, 1 when this index or request is not one the grid
+ * serves (call ngt_amd_search instead), -1 on error. */
+int ngt_amd_search_served(ngt_amd_index *index, const ngt_amd_search_params *params, const float *query,
+                          uint32_t *ids, float *dists, uint32_t *n, uint64_t *counters);
+/* Stop the serving grid now (it also stops by itself after a short idle time). */
+int ngt_amd_serve_stop(ngt_amd_index *index);
+/* Queries the serving grid answered and grids launched since the index was created. */
+int ngt_amd_serve_stats(ngt_amd_index *index, uint64_t *served, uint64_t *launches);
 int ngt_amd_search_device(ngt_amd_index *index, const ngt_amd_search_params *params,
                           const void *d_queries, uint64_t query_bytes, uint32_t nq,
                           const uint32_t *d_seeds, const uint64_t *d_seed_off, uint32_t *d_ids,

@@ -65,6 +65,9 @@ def declare(L):
         "ngt_amd_resolve_edge_size": (c_uint64, [vp, c_int64, c_float]),
         "ngt_amd_search": (c_int, [vp, POINTER(SearchParams), vp, c_uint32, vp, vp, vp, vp, vp, vp]),
         "ngt_amd_tree_seeds_device": (c_int, [vp, vp, c_uint64, c_uint32, c_uint32, vp, c_uint32, vp, vp]),
+        "ngt_amd_search_served": (c_int, [vp, POINTER(SearchParams), vp, vp, vp, vp, vp]),
+        "ngt_amd_serve_stop": (c_int, [vp]),
+        "ngt_amd_serve_stats": (c_int, [vp, vp, vp]),
         "ngt_amd_last_search_lookahead": (c_int, [vp]),
         "ngt_amd_qg_train_local_ngt": (c_int, [vp, c_uint64, c_uint32, c_uint32, vp]),
         "ngt_amd_search_device": (c_int, [vp, POINTER(SearchParams), vp, c_uint64, c_uint32, vp, vp, vp, vp,

@@ -551,6 +551,31 @@ enum { kGraphSearch = 0, kLinearSearch = 1 };
 static std::string single_query(CapiIndex* ix, int kind, const float* q, size_t size, float epsilon, float radius,
                                 int64_t edge_size, int seed_mode, std::vector<uint32_t>& ids,
                                 std::vector<float>& dists, uint32_t& n) {
+  // graph searches first try the resident serving grid (serve.cpp): answered
+  // as soon as this query finishes, without a launch or a batch to wait for
+  if (kind == kGraphSearch && size > 0 && size <= 64) {
+    std::shared_lock<std::shared_mutex> rd;
+    std::string e = sync_device(ix, rd);
+    if (!e.empty()) return e;
+    ngt_amd_search_params p{};
+    p.k = (uint32_t)size;
+    p.epsilon = epsilon;
+    p.radius = radius < 0.0f ? FLT_MAX : radius;
+    p.edge_size = edge_size;
+    p.seed_mode = seed_mode;
+    ids.resize(size);
+    dists.resize(size);
+    uint64_t c[NGT_AMD_COUNTERS_PER_QUERY];
+    const int r = ngt_amd_search_served(ix->dev, &p, q, ids.data(), dists.data(), &n, c);
+    if (r < 0) return amd_err();
+    if (r == 0) {
+      // the counters run_search reports (NeighborhoodGraph::search)
+      t_last_counters[0] = c[1];
+      t_last_counters[1] = c[4];
+      t_last_counters[2] = c[2];
+      return "";
+    }
+  }
   if (!ngt_amd::coalesce_enabled()) {
     std::vector<uint32_t> vn;
     std::string e = kind == kGraphSearch
@@ -1094,7 +1119,14 @@ bool ngt_get_coalesce_stats(NGTIndex index, uint64_t* batches, uint64_t* served,
     param_error(error, __FUNCTION__, "null argument");
     return false;
   }
-  coalescer_of(static_cast<CapiIndex*>(index))->stats(batches, served);
+  CapiIndex* ix = static_cast<CapiIndex*>(index);
+  coalescer_of(ix)->stats(batches, served);
+  // calls the resident serving grid answered count as served, its launches as batches
+  uint64_t s = 0, l = 0;
+  if (ix->dev && ngt_amd_serve_stats(ix->dev, &s, &l) == 0) {
+    *batches += l;
+    *served += s;
+  }
   return true;
 }
 

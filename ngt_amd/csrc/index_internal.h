@@ -161,6 +161,8 @@ struct GlibcRandHost {
 // ANNG construction state (build.cpp): the graph being built (host, sorted
 // edge lists), the DVP tree being built (HBM, fixed-capacity node arrays) and
 // the padded search adjacency the insertion searches read (HBM).
+struct Server;  // serve.cpp
+
 struct BuildState {
   int32_t edge_size_for_creation = 10, edge_size_for_search = 40, batch_size = 200, seed_size = 10;
   float epsilon_for_creation = 0.1f;
@@ -226,6 +228,7 @@ struct ngt_amd_index {
   DevBuf<float> in_border;
   DevBuf<uint64_t> leaf_off;
   uint32_t children = 5, root = 0;
+  uint64_t tree_version = 0;     // bumped whenever the tree changes
   // property
   int32_t edge_size_for_search = 0;
   int32_t dyn_base = 30, dyn_rate = 20;
@@ -239,6 +242,7 @@ struct ngt_amd_index {
   uint32_t spill_cap = 1u << 16;
   hipStream_t stream = nullptr;
   ngt_amd::BuildState* build = nullptr;    // ANNG construction (build.cpp)
+  ngt_amd::Server* serve = nullptr;        // resident single-query serving grid (serve.cpp)
   ~ngt_amd_index() {
     for (auto* c : ctxs) delete c;
     for (auto* c : calls) delete c;
@@ -275,6 +279,12 @@ struct CallGuard {
 int run_tree_seeds(ngt_amd_index* ix, SearchCtx* c, const void* d_queries, uint64_t query_bytes, uint32_t nq,
                    uint32_t k, int all_leaf_nodes, hipStream_t s);
 float coef_of(float epsilon);
+// the padded adjacency copy holding `need` edges per list (grown on demand;
+// caller holds ix->mu), and the edges a search of resolved edge size es reads
+int build_padded_adjacency(ngt_amd_index* ix, uint64_t need);
+uint64_t adjacency_need(const ngt_amd_index* ix, uint64_t es);
+// stop and free the serving grid (serve.cpp); no-op without one
+void serve_destroy(ngt_amd_index* ix);
 // GraphIndex::getRandomSeeds (Index.h:775-801) over the library's rand() stream
 // (a fresh process's glibc sequence, ngt_amd_srand)
 std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off);

@@ -93,6 +93,7 @@ extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distanc
 extern "C" void ngt_amd_index_destroy(ngt_amd_index* ix) {
   if (!ix) return;
   (void)hipSetDevice(ix->device);
+  serve_destroy(ix);  // the resident serving grid reads the index: stop it first
   if (ix->stream) (void)hipStreamSynchronize(ix->stream);
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
   delete ix;
@@ -145,7 +146,7 @@ static void note_graph_empty(ngt_amd_index* ix, const uint64_t* offsets, uint64_
 // reverse edges give some nodes hundreds) do not matter at its
 // EdgeSizeForSearch of 40.  W grows on demand; searches needing more than 256
 // edges of a list take the CSR path.
-static int build_padded_adjacency(ngt_amd_index* ix, uint64_t need) {
+int ngt_amd::build_padded_adjacency(ngt_amd_index* ix, uint64_t need) {
   if (need == 0 || need > 256) return 0;
   if (ix->adj.p && ix->adj_stride >= need) return 0;
   const uint64_t stride = (need + 15) & ~15ull;
@@ -166,7 +167,7 @@ static uint64_t max_degree_of(const uint64_t* h_offsets, uint64_t nrows) {
 }
 
 // edges a search with resolved edge size `es` reads of the widest list
-static uint64_t adjacency_need(const ngt_amd_index* ix, uint64_t es) {
+uint64_t ngt_amd::adjacency_need(const ngt_amd_index* ix, uint64_t es) {
   return std::min<uint64_t>(ix->max_degree, es);
 }
 
@@ -230,6 +231,7 @@ extern "C" int ngt_amd_index_set_tree(ngt_amd_index* ix, const void* in_pivot, u
   ix->children = children;
   ix->root = root;
   ix->has_tree = true;
+  ix->tree_version++;
   return 0;
 }
 
@@ -627,8 +629,8 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       const char* v = getenv("NGT_AMD_LAT");
       return !v || atoi(v) != 0;
     }();
-    if (lat_on && a.adj) {
-      const uint32_t cap = (uint32_t)std::min<uint64_t>(a.adj_stride, a.edge_size);
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(a.adj_stride, a.edge_size);
+    if (lat_on && a.adj && cap <= 256u && a.k <= 64u) {  // lists of <= 256 ids, results in one wave's registers
       SearchArgs b = a;
       b.lat_slots = cap <= 64 ? 32u : 16u;
       b.lat_tail = 4096u;

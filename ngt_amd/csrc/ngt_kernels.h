@@ -97,6 +97,54 @@ struct SearchArgs {
   uint32_t lat_tail;
 };
 
+// Serving form of the latency kernel (search_lat.hip, serve.cpp): a resident
+// grid takes single queries from a ring in pinned host memory as callers post
+// them and answers each one as soon as it finishes -- no launch per call and
+// no batch waiting for its slowest query.
+//
+// A request slot: ServeReqHdr, kServeMaxSeeds seed ids, then the prepared
+// query (dp floats) at kServeQueryOff; req_bytes apart.
+constexpr uint32_t kServeMaxSeeds = 128;
+constexpr uint32_t kServeQueryOff = 32 + 4 * kServeMaxSeeds;
+struct ServeReqHdr {
+  uint32_t seq;      // ticket + 1 once the slot is posted (host release store)
+  uint32_t k;        // SearchContainer::size, <= 64
+  uint32_t ns;       // random seeds in the slot (tree mode: descend instead)
+  uint32_t flags;
+  float coef;        // explorationCoefficient
+  float radius;      // sc.radius
+  uint32_t pad[2];
+};
+struct ServeResp {
+  uint32_t seq;      // ticket + 1 once answered (device system-scope release)
+  uint32_t n;
+  uint32_t err;      // the batch kernel's error bits for this query
+  uint32_t pad;
+  uint64_t counters[8];
+  uint32_t ids[64];
+  float dists[64];
+};
+struct ServeDevCtl {
+  uint32_t avail;    // tickets below this are posted (dispatcher)
+  uint32_t claimed;  // tickets below this are taken by a worker
+  uint32_t closing;  // the dispatcher has stopped: drain and leave
+  uint32_t pad;      // why it stopped: 1 asked, 2 idle, 3 lifetime
+};
+struct ServeArgs {
+  const uint8_t* ring;     // [nring][req_bytes] pinned host memory
+  uint64_t req_bytes;
+  ServeResp* resp;         // [nring] pinned host memory
+  uint32_t nring;
+  uint32_t workers;        // worker workgroups; block `workers` dispatches
+  ServeDevCtl* dctl;       // device memory
+  const uint32_t* stop;    // pinned host words: [0] stop dispatching, [1] tickets handed out
+  uint32_t start;          // first ticket of this launch
+  uint32_t use_tree;       // seeds from the tree (else the request's)
+  uint64_t idle_ticks;     // dispatcher leaves after this long without a post (100 MHz clock)
+  uint64_t life_ticks;     // ... or this long in all; workers' own bound is longer
+  TreeSeedArgs tree;
+};
+
 // lookahead targets per step of search_la.hip: mode 0 (throughput, one wave
 // per query), mode 1 (latency, eight waves per query)
 inline uint32_t la_targets(int mode) {
@@ -121,6 +169,7 @@ inline int la_wpe() {
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 uint32_t search_lat_lds_bytes(const SearchArgs& a);
 hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStream_t s);
+hipError_t launch_graph_serve_lat(const SearchArgs& a, const ServeArgs& sv, hipStream_t s);
 hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint32_t slots, hipStream_t s);
 
 struct LinearArgs {

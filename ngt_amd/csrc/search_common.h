@@ -32,6 +32,34 @@ __device__ __forceinline__ uint64_t stamp() {
 #define NGT_MARK(dst)
 #endif
 
+// glibc random(3) TYPE_3, for srand(leafID) (lib/NGT/Index.h:1555-1559): the
+// tree-seed thinning of ngt_tree_seed_kernel and of the serving kernel.
+struct GlibcRand {
+  uint32_t s[31];
+  int f, r;
+  __device__ void seed(uint32_t sd) {
+    int32_t word = (int32_t)(sd == 0 ? 1u : sd);
+    s[0] = (uint32_t)word;
+    for (int i = 1; i < 31; i++) {
+      int32_t hi = word / 127773, lo = word % 127773;
+      word = 16807 * lo - 2836 * hi;
+      if (word < 0) word += 2147483647;
+      s[i] = (uint32_t)word;
+    }
+    f = 3;
+    r = 0;
+    for (int i = 0; i < 310; i++) next();
+  }
+  __device__ int next() {
+    s[f] += s[r];
+    int res = (int)((s[f] >> 1) & 0x7fffffff);
+    f = f == 30 ? 0 : f + 1;
+    r = r == 30 ? 0 : r + 1;
+    return res;
+  }
+};
+
+
 // a wave-uniform double kept in SGPRs (the shuffle reductions leave the same
 // value in every lane, which the compiler cannot see)
 __device__ __forceinline__ double uniform_f64(double v) {

@@ -34,35 +34,6 @@ namespace ngt_amd {
 
 
 // ---------------------------------------------------------------------------
-// glibc random(3) TYPE_3, for srand(leafID) (lib/NGT/Index.h:1555-1559).
-// ---------------------------------------------------------------------------
-struct GlibcRand {
-  uint32_t s[31];
-  int f, r;
-  __device__ void seed(uint32_t sd) {
-    int32_t word = (int32_t)(sd == 0 ? 1u : sd);
-    s[0] = (uint32_t)word;
-    for (int i = 1; i < 31; i++) {
-      int32_t hi = word / 127773, lo = word % 127773;
-      word = 16807 * lo - 2836 * hi;
-      if (word < 0) word += 2147483647;
-      s[i] = (uint32_t)word;
-    }
-    f = 3;
-    r = 0;
-    for (int i = 0; i < 310; i++) next();
-  }
-  __device__ int next() {
-    s[f] += s[r];
-    int res = (int)((s[f] >> 1) & 0x7fffffff);
-    f = f == 30 ? 0 : f + 1;
-    r = r == 30 ? 0 : r + 1;
-    return res;
-  }
-};
-
-
-// ---------------------------------------------------------------------------
 // Batched comparator.  pair i: (query qidx[i], object oid[i]) -> out[i].
 // ---------------------------------------------------------------------------
 template <int M, typename T>

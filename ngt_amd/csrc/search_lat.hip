@@ -39,28 +39,36 @@ namespace ngt_amd {
 namespace {
 
 constexpr uint32_t kNoTag = 0xffu;  // head entry without a slot
-constexpr uint32_t kFree = 0u, kIssued = 1u, kTaken = 2u, kReady = 3u;
+constexpr uint32_t kFree = 0u, kIssued = 1u, kReady = 3u;
 
 struct LatCtl {
   uint32_t done;  // the commit wave has finished the query
   uint32_t qi;
-  uint32_t fthr;  // filter threshold of the current exploration radius
-  uint32_t fsq;   // sum q''^2
-  uint64_t sp[4]; // diagnostic build: speculation-wave cycles (adjacency, filter, exact, idle)
+  uint32_t quit;  // serving form: no more work for this workgroup
+  uint32_t k;     // this query's SearchContainer::size, coefficient, radius
+  float coef;
+  float radius;
+  uint32_t ns;    // serving form: seeds staged in the tail
+  uint32_t pad;
+  uint64_t sp[4]; // diagnostic build: speculation-wave cycles ([0] adjacency, [2] exact rows)
 };
 
 // one node's speculation: key (its unchecked-set key, the priority), state,
-// entries, list length
+// the claim word of its list parts (generation << 8 | parts taken), parts
+// finished, list length, fresh entries per part
 struct LatSlot {
   uint64_t key;
   uint32_t state;
-  uint32_t n;    // neighbours not yet visited when the list was read
-  uint32_t deg;  // list length read (getEdgeSize cap)
-  uint32_t pad[3];
+  uint32_t claim;
+  uint32_t done;
+  uint32_t deg;    // list length read (getEdgeSize cap), summed over the parts
+  uint32_t gen;    // issue generation (the commit wave's)
+  uint32_t pn[8];  // neighbours not yet visited when the part was read
+  uint32_t pad;
 };
 
 struct LatLayout {
-  uint32_t off_slot, off_eid, off_ed, off_tail, off_res, off_q, off_qb, off_nid, off_nd, off_hist, off_stg, off_bm,
+  uint32_t off_slot, off_eid, off_ed, off_tail, off_q, off_nid, off_nd, off_hist, off_bm,
       total;
   __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
   __host__ __device__ LatLayout(const SearchArgs& a, uint32_t cap, uint32_t waves) {
@@ -69,13 +77,10 @@ struct LatLayout {
     off_eid = o; o = up16(o + 4u * a.lat_slots * cap);
     off_ed = o; o = up16(o + 4u * a.lat_slots * cap);
     off_tail = o; o = up16(o + 8u * a.lat_tail);
-    off_res = o; o = up16(o + 8u * (a.k + 1));
     off_q = o; o = up16(o + 4u * (uint32_t)a.dp);
-    off_qb = o; o = up16(o + (uint32_t)a.dp);
     off_nid = o; o = up16(o + 256u);
     off_nd = o; o = up16(o + 256u);
     off_hist = o; o = up16(o + 256u);
-    off_stg = o; o = up16(o + 256u * waves);
     off_bm = o; o = up16(o + 4u * ((a.nrows + 31u) / 32u));
     total = o;
   }
@@ -172,33 +177,145 @@ __device__ __noinline__ uint64_t lat_select(const uint64_t* arr, uint32_t n, uin
   return lo + 1;  // never expected: the minimum alone
 }
 
+// ---- serving form (ngt_kernels.h ServeArgs) ---------------------------------
+// The dispatcher (one lane of the extra block): publishes each ticket whose
+// request slot the host has posted, in ticket order, until the host asks it
+// to stop, nothing was posted for idle_ticks, or life_ticks have passed;
+// then tells the workers to drain.
+__device__ void serve_dispatch(const ServeArgs& sv) {
+  if (lane_id() != 0) return;
+  uint32_t avail = sv.start;
+  const uint64_t t0 = wall_clock64();
+  uint64_t last = t0;
+  uint32_t why = 0;  // 1 asked to stop, 2 idle, 3 lifetime
+  for (;;) {
+    const uint64_t now = wall_clock64();
+    if (__hip_atomic_load(sv.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) why = 1;
+    // idle: nothing posted for idle_ticks and no ticket handed out unposted
+    // (a caller between taking its ticket and posting it)
+    else if (now - last > sv.idle_ticks &&
+             __hip_atomic_load(sv.stop + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == avail)
+      why = 2;
+    else if (now - t0 > sv.life_ticks) why = 3;
+    if (why) break;
+    const ServeReqHdr* h = reinterpret_cast<const ServeReqHdr*>(sv.ring + (uint64_t)(avail % sv.nring) * sv.req_bytes);
+    if (__hip_atomic_load(&h->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == avail + 1u) {
+      avail++;
+      __hip_atomic_store(&sv.dctl->avail, avail, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      last = now;
+      continue;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __hip_atomic_store(&sv.dctl->pad, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&sv.dctl->closing, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A worker's next ticket (returns false when it should leave): tickets
+// below `avail` are claimed in order; once the dispatcher closes, `avail` is
+// final.  Workers also leave on their own after life + idle + 1 s, so a grid
+// whose dispatcher block never got a CU still drains.
+__device__ bool serve_claim(const ServeArgs& sv, uint64_t t0, uint32_t& ticket) {
+  for (;;) {
+    uint32_t c = __hip_atomic_load(&sv.dctl->claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t av = __hip_atomic_load(&sv.dctl->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int32_t)(av - c) > 0) {
+      if (__hip_atomic_compare_exchange_strong(&sv.dctl->claimed, &c, c + 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        ticket = c;
+        return true;
+      }
+      continue;
+    }
+    if (__hip_atomic_load(&sv.dctl->closing, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      const uint32_t av2 = __hip_atomic_load(&sv.dctl->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t c2 = __hip_atomic_load(&sv.dctl->claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int32_t)(av2 - c2) > 0) continue;
+      return false;
+    }
+    if (wall_clock64() - t0 > sv.life_ticks + sv.idle_ticks + 100000000ull) return false;
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+// GraphAndTreeIndex::getSeedsFromTree for the serving form, on one wave: the
+// DVPTree leaf-mode descent (Tree.cpp:400-480, 531-563) and the leaf's
+// thinning (Index.h:1555-1562), as ngt_tree_seed_kernel does for a batch.
+// Leaf ids land in out[0, n) (LDS); returns n.
+__device__ uint32_t serve_tree_seeds(const TreeSeedArgs& t, const float* qlds, int dp, uint32_t k, uint32_t* out) {
+  const int lane = lane_id();
+  uint32_t node = t.root;
+  while (!(node & 0x80000000u)) {
+    const uint32_t iid = node & 0x7fffffffu;
+    float d = 0.f;
+    if (lane < 4) d = quad_distance<kL2, float>(qlds, row_ptr<float>(t.in_pivot, t.row_bytes, iid), dp, lane);
+    d = __shfl(d, 0, 64);
+    const float* borders = t.in_border + (uint64_t)iid * (t.children - 1);
+    uint32_t mid = 0;
+    for (; mid < t.children - 1; mid++)
+      if (d < borders[mid]) break;
+    node = t.in_child[(uint64_t)iid * t.children + mid];
+  }
+  const uint32_t lid = node & 0x7fffffffu;
+  const uint64_t b = t.leaf_off[lid];
+  uint32_t n = (uint32_t)(t.leaf_off[lid + 1] - b);
+  if (n > kServeMaxSeeds) n = kServeMaxSeeds;
+  for (uint32_t i = lane; i < n; i += 64) out[i] = t.leaf_ids[b + i];
+  __threadfence_block();
+  uint32_t ss = t.seed_size == 0 ? k : t.seed_size;
+  if (ss > k) ss = k;
+  if (t.all_leaf_nodes) ss = n;
+  if (n > ss) {
+    if (lane == 0) {
+      GlibcRand rnd;
+      rnd.seed(lid);
+      for (uint32_t i = n; i > ss; i--) {
+        const double random = ((double)rnd.next() + 1.0) / ((double)2147483647 + 2.0);
+        const uint32_t idx = (uint32_t)floor((double)i * random);
+        out[idx] = out[i - 1];
+      }
+    }
+    __threadfence_block();
+    n = ss;
+  }
+  return n;
+}
+
 }  // namespace
 
-// NCH = dp / 16; W waves (1 commit + W-1 speculation); RG = 16-entry filter
-// groups in flight per speculation wave (RG * 16 >= the list capacity)
-template <int NCH, int W, int RG>
-__global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs a) {
-  constexpr int E = 4 * NCH;  // filter-code bytes per lane of a quad
-  constexpr int NW = E / 8;   // 8-byte code words per lane
-  static_assert((NCH & 1) == 0, "whole 8-byte code words per lane");
+// NCH = dp / 16; W waves (1 commit + W-1 speculation).  A list of up to
+// `cap` ids is speculated as `parts` parts of 32 entries, each taken by one
+// speculation wave: its adjacency ids, then the exact rows of its fresh
+// neighbours (EG groups of 16 rows in flight) -- two dependent round trips.
+// SERVE: the resident serving form (queries from sv's ring, answers to its
+// response slots); otherwise one launch over a.nq prepared queries.
+template <int NCH, int W, bool SERVE>
+__global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs a, ServeArgs sv) {
+  constexpr int EG = 2;
+  if constexpr (SERVE) {
+    if (blockIdx.x == sv.workers) {
+      if (threadIdx.x < 64) serve_dispatch(sv);
+      return;
+    }
+  }
+  const uint64_t t_start = SERVE ? wall_clock64() : 0ull;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t cap = (uint32_t)(a.adj_stride < a.edge_size ? a.adj_stride : a.edge_size);
+  constexpr uint32_t span = 32u;  // ids per part: one group of EG x 16 rows
+  const uint32_t parts = (cap + span - 1u) / span;  // <= 8
   const LatLayout lay(a, cap, W);
   LatCtl* ctl = reinterpret_cast<LatCtl*>(smem);
   LatSlot* slots = reinterpret_cast<LatSlot*>(smem + lay.off_slot);
   uint32_t* eid = reinterpret_cast<uint32_t*>(smem + lay.off_eid);
   float* ed = reinterpret_cast<float*>(smem + lay.off_ed);
   uint64_t* tail = reinterpret_cast<uint64_t*>(smem + lay.off_tail);
-  uint64_t* res = reinterpret_cast<uint64_t*>(smem + lay.off_res);
   float* qlds = reinterpret_cast<float*>(smem + lay.off_q);
-  uint8_t* qb = smem + lay.off_qb;
   uint32_t* nid = reinterpret_cast<uint32_t*>(smem + lay.off_nid);
   float* nd = reinterpret_cast<float*>(smem + lay.off_nd);
   uint32_t* bm = reinterpret_cast<uint32_t*>(smem + lay.off_bm);
   // threshold-selection counters: not nid/nd, which hold the accept step's
   // staged candidates when a full tail makes room in the middle of it
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lay.off_hist);
-  uint32_t* stg = reinterpret_cast<uint32_t*>(smem + lay.off_stg) + 64 * (threadIdx.x >> 6);  // per wave
 
   const int lane = lane_id();
   const int wave = (int)(threadIdx.x >> 6);
@@ -206,45 +323,89 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
   constexpr uint32_t NT = 64u * W;
   const uint32_t bm_words = (a.nrows + 31u) / 32u;
   const uint32_t nslots = a.lat_slots;
-  const float fa = a.fparams[0], fb = a.fparams[1], fe = a.fparams[2];
-  const double finv_b = 1.0 / (double)fb;
   const uint32_t wg = blockIdx.x;
   uint64_t* spill = a.spill + (uint64_t)wg * a.spill_cap;
-  const uint32_t k = a.k;
   const int g = lane & 3, rs = lane >> 2;
 
   for (;;) {
-    if (tid == 0) ctl->qi = atomicAdd(a.work, 1u);
+    if (tid == 0) {
+      if constexpr (SERVE) {
+        uint32_t t = 0;
+        ctl->quit = serve_claim(sv, t_start, t) ? 0u : 1u;
+        ctl->qi = t;
+      } else {
+        ctl->qi = atomicAdd(a.work, 1u);
+        ctl->quit = 0u;
+      }
+    }
     __syncthreads();
     const uint32_t qi = ctl->qi;
-    if (qi >= a.nq) break;
+    if (SERVE ? ctl->quit != 0u : qi >= a.nq) break;
+    // the serving form's request slot (pinned host memory, posted before its
+    // ticket was published: acquire at system scope before reading it)
+    const uint8_t* req = SERVE ? sv.ring + (uint64_t)(qi % sv.nring) * sv.req_bytes : nullptr;
+    if constexpr (SERVE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 
     // ---- per-query init (every wave) -------------------------------------
     {
       uint4* b4 = reinterpret_cast<uint4*>(bm);
       for (uint32_t i = tid; i < (bm_words + 3) / 4; i += NT) b4[i] = make_uint4(0, 0, 0, 0);
-      const uint4* s = reinterpret_cast<const uint4*>(a.queries + (uint64_t)qi * a.query_bytes);
+      const uint4* s = reinterpret_cast<const uint4*>(SERVE ? req + kServeQueryOff
+                                                            : a.queries + (uint64_t)qi * a.query_bytes);
       uint4* d = reinterpret_cast<uint4*>(qlds);
       for (uint32_t i = tid; i < (uint32_t)a.dp / 4; i += NT) d[i] = s[i];
-      for (uint32_t i = tid; i < nslots; i += NT) slots[i].state = kFree;
+      for (uint32_t i = tid; i < nslots; i += NT) {
+        slots[i].state = kFree;
+        slots[i].claim = 0u;
+        slots[i].gen = 0u;
+      }
       if (tid == 0) {
         ctl->done = 0u;
         ctl->sp[0] = ctl->sp[1] = ctl->sp[2] = ctl->sp[3] = 0ull;
+        if constexpr (SERVE) {
+          const ServeReqHdr* h = reinterpret_cast<const ServeReqHdr*>(req);
+          ctl->k = h->k;
+          ctl->coef = h->coef;
+          ctl->radius = h->radius;
+          ctl->ns = h->ns;
+        } else {
+          ctl->k = a.k;
+          ctl->coef = a.coef;
+          ctl->radius = a.radius;
+        }
+      }
+      // the request's random seeds, staged in the (still empty) tail
+      if constexpr (SERVE) {
+        if (!sv.use_tree)
+          for (uint32_t i = tid; i < kServeMaxSeeds; i += NT)
+            reinterpret_cast<uint32_t*>(tail)[i] = reinterpret_cast<const uint32_t*>(req + 32)[i];
       }
     }
     __syncthreads();
+    const uint32_t k = ctl->k;
+    const float coefq = ctl->coef, radq = ctl->radius;
 
     if (wave == 0) {
       // =================== the commit wave ===================================
-      uint32_t fsq = 0;
-      double frq = 0.0;
-      filter_query(qlds, a.dp, fa, fb, qb, fsq, frq);
       uint32_t nres = 0, maxq = 0;
+      // the result set (Graph.cpp:471-483's ResultSet, k <= 64) in registers:
+      // lane i holds the i-th smallest (distance, id) key
+      uint64_t rk = ~0ull;
+      auto res_push = [&](uint64_t key) {
+        const uint32_t pos = (uint32_t)__popcll(ballot64((uint32_t)lane < nres && rk < key));
+        if (pos >= k) return;
+        const uint64_t up = wave_up1_u64(rk);
+        if ((uint32_t)lane > pos) rk = up;
+        if ((uint32_t)lane == pos) rk = key;
+        nres = nres + 1 < k ? nres + 1 : k;
+      };
       uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0;
+      (void)nwait;
       // diagnostic build only: shader-clock totals per phase
       uint64_t t_pop = 0, t_wait = 0, t_list = 0, t_feed = 0, t_last = 0;
       (void)t_pop; (void)t_wait; (void)t_list; (void)t_feed; (void)t_last;
-      float radius = a.radius;
+      float radius = radq;
+      uint32_t qerr = 0;  // the batch kernel's error bits, this query's
       float expr = 0.f;
       // unchecked set: head (registers, sorted, hn keys) < B <= tail (LDS,
       // ntail keys) < T <= spill (HBM, nspill keys)
@@ -256,12 +417,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       uint64_t orphan = 0ull;                                             // issued, no longer in the head
       const uint32_t F = nslots < 16u ? nslots : 16u;                     // head entries kept speculated
 
-      auto set_fthr = [&]() {
-        if (lane == 0) ctl->fthr = filter_threshold(expr, (double)fe, finv_b, frq);
-      };
       auto spill_push = [&](uint64_t key) {
         if (nspill >= a.spill_cap) {
-          if (lane == 0) atomicOr(a.error, 1);
+          qerr |= 1u;
         } else {
           if (lane == 0) spill[nspill] = key;
           nspill++;
@@ -298,7 +456,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           const uint64_t mm = ballot64(mv), km = ballot64(kp);
           const uint32_t nm = (uint32_t)__popcll(mm);
           if (nspill + nm > a.spill_cap) {
-            if (lane == 0) atomicOr(a.error, 1);
+            qerr |= 1u;
           } else if (mv) {
             spill[nspill + mbcnt(mm)] = key;
           }
@@ -308,7 +466,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           __builtin_amdgcn_wave_barrier();
           out += (uint32_t)__popcll(km);
         }
-        if ((out == 0u || out > keep) && lane == 0) atomicOr(a.error, 32);  // selection check
+        if (out == 0u || out > keep) qerr |= 32u;  // selection check
         ntail = out;
         T = l;
       };
@@ -392,7 +550,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         nspill = out;
         T = nspill ? l : ~0ull;
-        if ((ntail == 0u || ntail > want) && lane == 0) atomicOr(a.error, 64);  // selection check
+        if (ntail == 0u || ntail > want) qerr |= 64u;  // selection check
       };
       auto refill_head = [&]() {
         if (ntail == 0 && nspill != 0) refill_tail();
@@ -424,7 +582,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           v = (uint32_t)lane < got ? st64[lane] : ~0ull;
         }
         ntail = out;
-        if ((got == 0u || got > 64u) && lane == 0) atomicOr(a.error, 128);  // selection check
+        if (got == 0u || got > 64u) qerr |= 128u;  // selection check
         // bitonic sort of the 64 lanes (ascending; empty lanes hold ~0)
 #pragma unroll
         for (int kk = 2; kk <= 64; kk <<= 1) {
@@ -477,7 +635,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           reap();
           if (freem != 0ull) break;
           if (spin > (1u << 24)) {
-            if (lane == 0) atomicOr(a.error, 16);
+            qerr |= 16u;
             stuck = true;
             return 0u;
           }
@@ -485,9 +643,19 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         const uint32_t s = (uint32_t)(__ffsll((long long)freem) - 1);
         freem &= ~(1ull << s);
-        if (lane == 0) slots[s].key = key;
+        const uint32_t gen = (slots[s].gen + 1u) & 0xffffffu;
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) lds_store_rel(&slots[s].state, kIssued);
+        if (lane == 0) {
+          slots[s].key = key;
+          slots[s].done = 0u;
+          slots[s].deg = 0u;
+          slots[s].gen = gen;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          lds_store_rel(&slots[s].claim, gen << 8);
+          lds_store_rel(&slots[s].state, kIssued);
+        }
         return s;
       };
       // speculation for the first F head entries that have none
@@ -503,43 +671,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           if (lane == l) ht = s;
         }
       };
-      auto push_batch = [&](uint64_t bm_) {
-        uint64_t r = bm_;
-        while (r) {
-          const int j = __ffsll((long long)r) - 1;
-          r &= r - 1;
-          insert_key(make_key(nd[j], nid[j]));
-        }
-      };
-      // accept `me` staged candidates (nid/nd, all fresh) in neighbour order
-      // (Graph.cpp:471-483), the sequential outcome exactly
-      auto accept = [&](uint32_t me) {
-        const float dl = (uint32_t)lane < me ? nd[lane] : 0.f;
-        const bool inl = (uint32_t)lane < me;
-        uint64_t okmask = ballot64(inl && dl <= expr);
-        while (okmask) {
-          const uint64_t rmask = okmask & ballot64(inl && dl <= radius);
-          if (rmask == 0ull) {
-            push_batch(okmask);
-            break;
-          }
-          const int j = __ffsll((long long)rmask) - 1;
-          push_batch(okmask & ((1ull << j) - 1ull));
-          const uint64_t key = make_key(nd[j], nid[j]);
-          insert_key(key);
-          res_insert(res, nres, k, key);
-          if (nres >= k) {
-            radius = key_dist(res[k - 1]);
-            expr = __fmul_rn(a.coef, radius);
-            set_fthr();
-          }
-          __builtin_amdgcn_wave_barrier();
-          okmask &= ~((2ull << j) - 1ull);
-          okmask &= ballot64(inl && dl <= expr);
-        }
-      };
-
-      // the same accept on candidates held in registers: lanes of `cmask`
+      // accept the candidates held in registers in neighbour order
+      // (Graph.cpp:471-483), the sequential outcome exactly: lanes of `cmask`
       // (neighbour order = lane order), ids in idv, distances in dv -- no LDS
       // staging on the commit path
       auto accept_reg = [&](uint64_t cmask, uint32_t idv, float dv) {
@@ -563,11 +696,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           const uint64_t key = make_key(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), j)),
                                         (uint32_t)__builtin_amdgcn_readlane((int)idv, j));
           insert_key(key);
-          res_insert(res, nres, k, key);
+          res_push(key);
           if (nres >= k) {
-            radius = key_dist(res[k - 1]);
-            expr = __fmul_rn(a.coef, radius);
-            set_fthr();
+            radius = key_dist(readlane_u64(rk, (int)k - 1));
+            expr = __fmul_rn(coefq, radius);
           }
           __builtin_amdgcn_wave_barrier();
           okmask &= ~((2ull << j) - 1ull);
@@ -576,12 +708,22 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       };
 
       // ---- setupDistances + setupSeeds (Graph.cpp:293-367) ----------------
-      const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
-      ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
-      expr = __fmul_rn(a.coef, radius);
+      // (the serving form's seeds sit in the tail: the head takes the first 64
+      // keys, so no key reaches the tail before the last chunk is read)
+      uint64_t sb = 0;
+      const uint32_t* sp;
+      if constexpr (SERVE) {
+        sp = reinterpret_cast<const uint32_t*>(tail);
+        ns = sv.use_tree ? serve_tree_seeds(sv.tree, qlds, a.dp, k, reinterpret_cast<uint32_t*>(tail)) : ctl->ns;
+      } else {
+        sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
+        ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
+        sp = a.seeds;
+      }
+      expr = __fmul_rn(coefq, radius);
       for (uint32_t base = 0; base < ns; base += 64) {
         const uint32_t m = ns - base < 64 ? (uint32_t)(ns - base) : 64u;
-        if ((uint32_t)lane < m) nid[lane] = a.seeds[sb + base + lane];
+        if ((uint32_t)lane < m) nid[lane] = sp[sb + base + lane];
         __builtin_amdgcn_wave_barrier();
         eval_l2f_fast<NCH, 1>(qlds, a.rows, a.row_bytes, nid, nd, (int)m);
         __builtin_amdgcn_wave_barrier();
@@ -594,15 +736,13 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           const float d = nd[j];
           const uint64_t key = make_key(d, nid[j]);
           insert_key(key);
-          if (d <= a.radius) res_insert(res, nres, k, key);
+          if (d <= radq) res_push(key);
         }
         __builtin_amdgcn_wave_barrier();
       }
       ndist = ns;
-      if (nres >= k) radius = key_dist(res[k - 1]);
-      expr = __fmul_rn(a.coef, radius);
-      if (lane == 0) ctl->fsq = fsq;
-      set_fthr();
+      if (nres >= k) radius = key_dist(readlane_u64(rk, (int)k - 1));
+      expr = __fmul_rn(coefq, radius);
       feed();
 
       // ---- best-first loop (Graph.cpp:430-486) ------------------------------
@@ -625,7 +765,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (lds_load_acq(&slots[tag].state) != kReady) nstall++;
         for (uint32_t spin = 0; lds_load_acq(&slots[tag].state) != kReady; spin++) {
           if (spin > (1u << 24)) {
-            if (lane == 0) atomicOr(a.error, 16);
+            qerr |= 16u;
             stuck = true;
             break;
           }
@@ -633,38 +773,36 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         if (stuck) break;
         NGT_MARK(t_wait);
-        const uint32_t n = slots[tag].n;
         nexp++;
         nedge += slots[tag].deg;
-        const uint32_t* sid = eid + tag * cap;
-        const float* sd = ed + tag * cap;
-        // the whole list (<= 256 entries: 4 per lane) in one pass -- every
-        // load issued before the first visited test, every test before the
-        // marks -- then the accepts in neighbour order.  Ids of one list are
-        // distinct, so testing and marking them in parallel is the sequential
-        // outcome.
+        // the parts of the list in order, two per pass (lanes 0-31 part p,
+        // 32-63 part p+1; each part compacted in list order, so lane order
+        // is neighbour order): visited test, mark, then the accepts in
+        // neighbour order.  Ids of one list are distinct, so testing and
+        // marking them in parallel is the sequential outcome.  Speculation
+        // for the accepted keys that reach the head's front is handed out
+        // after every pass, not only after the list.
         {
-          uint32_t id4[4];
-          float d4[4];
-          bool f4[4];
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            const uint32_t e = 64u * c + (uint32_t)lane;
-            id4[c] = e < n ? sid[e] : 0u;
-            d4[c] = e < n ? sd[e] : 0.f;
-          }
-#pragma unroll
-          for (int c = 0; c < 4; c++) f4[c] = id4[c] != 0u && !bm_test(bm, id4[c]);
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            if (64u * c >= n) break;
-            if (f4[c]) atomicOr(bm + (id4[c] >> 5), 1u << (id4[c] & 31));
-            ndist += (uint32_t)__popcll(ballot64(f4[c]));
-            nexact += (uint32_t)__popcll(ballot64(f4[c] && d4[c] != __builtin_huge_valf()));
-            // candidates within the radius (d = +inf: rejected by the bound),
-            // accepted in neighbour order against the shrinking radius
-            const uint64_t km = ballot64(f4[c] && d4[c] <= expr);
-            if (km) accept_reg(km, id4[c], d4[c]);
+          const uint32_t* sid = eid + tag * cap;
+          const float* sd = ed + tag * cap;
+          const uint32_t half = (uint32_t)lane >> 5, sub = (uint32_t)lane & 31u;
+#pragma unroll 1
+          for (uint32_t p = 0; p < parts; p += 2) {
+            const uint32_t pp = p + half;
+            const uint32_t np = pp < parts ? slots[tag].pn[pp] : 0u;
+            const bool in = sub < np;
+            const uint32_t idv = in ? sid[pp * span + sub] : 0u;
+            const float dv = in ? sd[pp * span + sub] : 0.f;
+            const bool f = idv != 0u && !bm_test(bm, idv);
+            if (f) atomicOr(bm + (idv >> 5), 1u << (idv & 31));
+            const uint32_t nf = (uint32_t)__popcll(ballot64(f));
+            ndist += nf;
+            nexact += nf;
+            const uint64_t km = ballot64(f && dv <= expr);
+            if (km) {
+              accept_reg(km, idv, dv);
+              if (p + 2u < parts) feed();
+            }
           }
         }
         if (lane == 0) slots[tag].state = kFree;
@@ -678,37 +816,51 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       if (lane == 0) lds_store_rel(&ctl->done, 1u);
 
       // ---- results (moveFrom: ascending (distance, id), ObjectSpace.h:49-57)
-      for (uint32_t i = lane; i < nres; i += 64) {
-        a.out_ids[(uint64_t)qi * k + i] = key_id(res[i]);
-        a.out_dists[(uint64_t)qi * k + i] = key_dist(res[i]);
-      }
-      if (lane == 0) {
-        a.out_n[qi] = nres;
-        if (a.counters) {
-          uint64_t* c = a.counters + (uint64_t)qi * 8;
-          c[0] = ndist;
-          c[1] = ndist - ns;
-          c[2] = nexp;
-          c[3] = nstall;  // pops that waited for their list (nwait of them: not yet handed out)
-          c[4] = nedge;
-          c[5] = maxq;
-          c[6] = nexact;
-          c[7] = ns;
+      uint64_t cv[8] = {ndist, ndist - ns, nexp, nstall, nedge, maxq, nexact, ns};
 #ifdef NGT_AMD_STAMPS
-          // phase cycles: [5] pop (+ refills, issue), [6] wait for the list,
-          // [1] list + accept, [7] feeding the speculation; [3] nwait
-          c[5] = t_pop;
-          c[6] = t_wait;
-          c[1] = t_list;
-          c[7] = t_feed;
-          c[3] = nwait;
-          // speculation waves, summed over the waves: [0] adjacency + visited
-          // pre-test, [4] filter codes, [2] exact rows (expansions: nexp)
-          __builtin_amdgcn_s_waitcnt(0);
-          c[0] = ctl->sp[0];
-          c[4] = ctl->sp[1];
-          c[2] = ctl->sp[2];
+      // phase cycles: [5] pop (+ refills, issue), [6] wait for the list,
+      // [1] list + accept, [7] feeding the speculation; [3] nwait; the
+      // speculation waves' sums: [0] adjacency + visited pre-test, [2] exact rows
+      __builtin_amdgcn_s_waitcnt(0);
+      cv[5] = t_pop;
+      cv[6] = t_wait;
+      cv[1] = t_list;
+      cv[7] = t_feed;
+      cv[3] = nwait;
+      cv[0] = ctl->sp[0];
+      cv[4] = ctl->sp[1];
+      cv[2] = ctl->sp[2];
 #endif
+      if constexpr (SERVE) {
+        // the answer, then its ticket (system-scope release: the caller polls
+        // the slot in host memory)
+        ServeResp* r = sv.resp + (qi % sv.nring);
+        if ((uint32_t)lane < nres) {
+          r->ids[lane] = key_id(rk);
+          r->dists[lane] = key_dist(rk);
+        }
+        if (lane == 0) {
+          r->n = nres;
+          r->err = qerr;
+#pragma unroll
+          for (int i = 0; i < 8; i++) r->counters[i] = cv[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (lane == 0) __hip_atomic_store(&r->seq, qi + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        if ((uint32_t)lane < nres) {
+          a.out_ids[(uint64_t)qi * k + lane] = key_id(rk);
+          a.out_dists[(uint64_t)qi * k + lane] = key_dist(rk);
+        }
+        if (lane == 0) {
+          a.out_n[qi] = nres;
+          if (qerr) atomicOr(a.error, (int)qerr);
+          if (a.counters) {
+            uint64_t* c = a.counters + (uint64_t)qi * 8;
+#pragma unroll
+            for (int i = 0; i < 8; i++) c[i] = cv[i];
+          }
         }
       }
     } else {
@@ -717,51 +869,42 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (lds_load_acq(&ctl->done)) break;
         // the issued slot with the smallest key
         const uint32_t st = (uint32_t)lane < nslots ? lds_load_acq(&slots[lane].state) : kFree;
-        const uint64_t cand = st == kIssued ? slots[lane].key : ~0ull;
+        const uint32_t cw = (uint32_t)lane < nslots ? lds_load_acq(&slots[lane].claim) : 0u;
+        const uint64_t cand = st == kIssued && (cw & 0xffu) < parts ? slots[lane].key : ~0ull;
         const uint64_t m = uniform_u64_lat(wave_min_u64(cand));
         if (m == ~0ull) {
           if (lds_load_acq(&ctl->done)) break;
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        const uint32_t s = (uint32_t)(__ffsll((long long)ballot64(cand == m)) - 1);
-        uint32_t old = 0;
-        if (lane == 0) old = atomicCAS(&slots[s].state, kIssued, kTaken);
-        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)old) != kIssued) continue;  // another wave took it
-        const uint32_t node = key_id(m);
+        const int sl = __ffsll((long long)ballot64(cand == m)) - 1;
+        // claim the next part of that list: CAS on (generation, parts taken),
+        // so a claim from before the slot's reissue cannot succeed
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, sl);
+        uint32_t got = 0;
+        if (lane == 0) {
+          uint32_t expect = w;
+          got = __hip_atomic_compare_exchange_strong(&slots[sl].claim, &expect, w + 1u, __ATOMIC_ACQUIRE,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+        }
+        if (!__builtin_amdgcn_readfirstlane((int)got)) continue;  // another wave took it
+        const uint32_t part = w & 0xffu;
+        const uint32_t node = key_id(slots[sl].key);
 #ifdef NGT_AMD_STAMPS
         uint64_t st0 = stamp();
 #endif
-        uint32_t* sid = eid + s * cap;
-        float* sd = ed + s * cap;
-        uint32_t n = 0, deg = 0;
-        // the filter threshold of the current exploration radius (it only
-        // shrinks: a neighbour the bound rejects is outside the radius at
-        // commit time too)
-        const uint32_t fthr = lds_load_acq(&ctl->fthr), fsq = ctl->fsq;
-        uint2 q[NW];
-        {
-          const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
-#pragma unroll
-          for (int w = 0; w < NW; w++) q[w] = qp[w];
-        }
-        {
-        // adjacency row: the first min(degree, edgeSize) ids (Graph.cpp:436-439)
-        uint32_t r0, r1, r2, r3;
-        load_adj_row(a.adj + (uint64_t)node * a.adj_stride, cap, r0, r1, r2, r3);        deg = (uint32_t)(__popcll(ballot64(r0 != 0u)) + __popcll(ballot64(r1 != 0u)) +
-                                        __popcll(ballot64(r2 != 0u)) + __popcll(ballot64(r3 != 0u)));
-        // neighbours not visited yet, compacted in list order
-        {
-          const uint32_t rr[4] = {r0, r1, r2, r3};
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            if ((uint32_t)(64 * c) >= deg) break;
-            const bool f = rr[c] != 0u && !bm_test(bm, rr[c]);
-            const uint64_t fm = ballot64(f);
-            if (f) sid[n + mbcnt(fm)] = rr[c];
-            n += (uint32_t)__popcll(fm);
-          }
-        }
+        // this part's adjacency ids (the first min(degree, edgeSize) of the
+        // list, Graph.cpp:436-439) and the ones not visited yet, in order
+        const uint32_t p0 = part * span;
+        const uint32_t len = cap - p0 < span ? cap - p0 : span;
+        const uint32_t id = (uint32_t)lane < len ? a.adj[(uint64_t)node * a.adj_stride + p0 + lane] : 0u;
+        const uint32_t live = (uint32_t)__popcll(ballot64(id != 0u));
+        const bool fresh = id != 0u && !bm_test(bm, id);
+        const uint64_t fm = ballot64(fresh);
+        const uint32_t np = (uint32_t)__popcll(fm);
+        uint32_t* sid = eid + sl * cap + p0;
+        float* sd = ed + sl * cap + p0;
+        if (fresh) sid[mbcnt(fm)] = id;
         __builtin_amdgcn_wave_barrier();
 #ifdef NGT_AMD_STAMPS
         {
@@ -770,80 +913,28 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           st0 = t1;
         }
 #endif
-        // filter codes of every entry (quad per entry), RG groups of 16 in
-        // flight; the threshold of the current exploration radius (it only
-        // shrinks: a rejected neighbour is outside the radius at commit too)
-        for (uint32_t base = 0; base < n; base += 16u * RG) {
-          uint2 c[RG][NW];
-#pragma unroll
-          for (int j = 0; j < RG; j++) {
-            const uint32_t e = base + 16u * j + (uint32_t)rs;
-            const uint32_t id = e < n ? sid[e] : 0u;
-            const uint2* cp = reinterpret_cast<const uint2*>(a.fcodes + (uint64_t)id * (4 * E)) + g * NW;
-            if (base + 16u * j < n) {
-#pragma unroll
-              for (int w = 0; w < NW; w++) c[j][w] = cp[w];
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < RG; j++) {
-            if (base + 16u * j >= n) continue;
-            uint32_t qc = 0u, cc = 0u;
-#pragma unroll
-            for (int w = 0; w < NW; w++) {
-              qc = __builtin_amdgcn_udot4(q[w].x, c[j][w].x, qc, false);
-              qc = __builtin_amdgcn_udot4(q[w].y, c[j][w].y, qc, false);
-              cc = __builtin_amdgcn_udot4(c[j][w].x, c[j][w].x, cc, false);
-              cc = __builtin_amdgcn_udot4(c[j][w].y, c[j][w].y, cc, false);
-            }
-            const uint32_t S = fsq + quad_sum_u32(cc - 2u * qc);
-            const uint32_t e = base + 16u * j + (uint32_t)rs;
-            // survivors: -1 until their exact distance lands; the rest +inf
-            if (g == 0 && e < n) sd[e] = S <= fthr ? -1.f : __builtin_huge_valf();
-          }
-        }
-        }
-        __builtin_amdgcn_wave_barrier();
-#ifdef NGT_AMD_STAMPS
-        {
-          const uint64_t t1 = stamp();
-          if (lane == 0) atomicAdd((unsigned long long*)&ctl->sp[1], (unsigned long long)(t1 - st0));
-          st0 = t1;
-        }
-#endif
-        // exact comparator distances of the survivors (PrimitiveComparator::
-        // compareL2 through l2_fold_rows), 16 rows per wave step
+        // the comparator's exact distances of those neighbours
+        // (PrimitiveComparator::compareL2 through l2_fold_rows): a quad per
+        // row, EG groups of 16 rows in flight
         {
           const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
-          uint32_t nsv = 0;
-          for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-            const uint32_t e = e0 + (uint32_t)lane;
-            const bool sv = e < n && sd[e] < 0.f;
-            const uint64_t sm = ballot64(sv);
-            __builtin_amdgcn_wave_barrier();
-            if (sv && nsv + mbcnt(sm) < 64u) stg[nsv + mbcnt(sm)] = e;
-            __builtin_amdgcn_wave_barrier();
-            nsv += (uint32_t)__popcll(sm);
-            if (nsv >= 48u || e0 + 64 >= n) {
-              const uint32_t m_ = nsv < 64u ? nsv : 64u;
-              for (uint32_t r0 = 0; r0 < m_; r0 += 16) {
-                const uint32_t rr = r0 + (uint32_t)rs;
-                const uint32_t pos = rr < m_ ? stg[rr] : 0u;
-                const uint32_t id = rr < m_ ? sid[pos] : 0u;
-                const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)id * a.row_bytes) + g;
-                float4 v[NCH];
+          for (uint32_t r0 = 0; r0 < np; r0 += 16u * EG) {
+            float4 v[EG][NCH];
 #pragma unroll
-                for (int i = 0; i < NCH; i++) v[i] = x[4 * i];
-                const float d = l2_fold_rows<NCH>(qq, v);
-                if (g == 0 && rr < m_) sd[pos] = d;
-              }
-              __builtin_amdgcn_wave_barrier();
-              // survivors past the 64 staged ones: a later pass of this loop
-              // sees them still at -1
-              if (nsv > 64u) {
-                e0 -= 64;  // re-scan this chunk for the rest
-              }
-              nsv = 0;
+            for (int j = 0; j < EG; j++) {
+              if (r0 + 16u * j >= np) continue;
+              const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
+              const uint32_t rid = rr < np ? sid[rr] : 0u;
+              const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)rid * a.row_bytes) + g;
+#pragma unroll
+              for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
+            }
+#pragma unroll
+            for (int j = 0; j < EG; j++) {
+              if (r0 + 16u * j >= np) continue;
+              const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
+              const float d = l2_fold_rows<NCH>(qq, v[j]);
+              if (g == 0 && rr < np) sd[rr] = d;
             }
           }
         }
@@ -852,11 +943,15 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (lane == 0) atomicAdd((unsigned long long*)&ctl->sp[2], (unsigned long long)(stamp() - st0));
 #endif
         if (lane == 0) {
-          slots[s].n = n;
-          slots[s].deg = deg;
+          slots[sl].pn[part] = np;
+          atomicAdd(&slots[sl].deg, live);
         }
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) lds_store_rel(&slots[s].state, kReady);
+        uint32_t prev = 0;
+        if (lane == 0)
+          prev = __hip_atomic_fetch_add(&slots[sl].done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
+        if (prev + 1u == parts && lane == 0) lds_store_rel(&slots[sl].state, kReady);  // the last part completes it
       }
     }
     __syncthreads();
@@ -874,22 +969,37 @@ uint32_t search_lat_lds_bytes(const SearchArgs& a) {
 
 hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStream_t s) {
   if (a.nq == 0) return hipSuccess;
-  if ((a.dp != 128 && a.dp != 96) || !a.adj || !a.fcodes) return hipErrorNotSupported;
   const uint32_t cap = (uint32_t)(a.adj_stride < a.edge_size ? a.adj_stride : a.edge_size);
+  // parts of 32 entries, at most 8 per list; results in one wave's registers
+  if ((a.dp != 128 && a.dp != 96) || !a.adj || cap > 256u || a.k > 64u) return hipErrorNotSupported;
   const size_t lds = search_lat_lds_bytes(a);
-#define LAT(NCH, RG)                                                                                            \
+  const ServeArgs none{};
+#define LAT(NCH)                                                                                                \
   do {                                                                                                          \
-    auto kern = ngt_graph_search_lat_kernel<NCH, 8, RG>;                                                        \
+    auto kern = ngt_graph_search_lat_kernel<NCH, 8, false>;                                                     \
     hipError_t e_ = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
     if (e_ != hipSuccess) return e_;                                                                            \
-    hipLaunchKernelGGL(kern, dim3(slots), dim3(512), lds, s, a);                                                \
+    hipLaunchKernelGGL(kern, dim3(slots), dim3(512), lds, s, a, none);                                          \
   } while (0)
-  if (a.dp == 128) {
-    if (cap <= 64) LAT(8, 4); else LAT(8, 9);
-  } else {
-    if (cap <= 64) LAT(6, 4); else LAT(6, 10);
-  }
+  if (a.dp == 128) LAT(8); else LAT(6);
 #undef LAT
+  return hipGetLastError();
+}
+
+hipError_t launch_graph_serve_lat(const SearchArgs& a, const ServeArgs& sv, hipStream_t s) {
+  const uint32_t cap = (uint32_t)(a.adj_stride < a.edge_size ? a.adj_stride : a.edge_size);
+  if ((a.dp != 128 && a.dp != 96) || !a.adj || cap > 256u || sv.workers == 0 || sv.nring == 0)
+    return hipErrorNotSupported;
+  const size_t lds = search_lat_lds_bytes(a);
+#define SRV(NCH)                                                                                                \
+  do {                                                                                                          \
+    auto kern = ngt_graph_search_lat_kernel<NCH, 8, true>;                                                      \
+    hipError_t e_ = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    if (e_ != hipSuccess) return e_;                                                                            \
+    hipLaunchKernelGGL(kern, dim3(sv.workers + 1), dim3(512), lds, s, a, sv);                                   \
+  } while (0)
+  if (a.dp == 128) SRV(8); else SRV(6);
+#undef SRV
   return hipGetLastError();
 }
 

@@ -133,6 +133,31 @@ class DeviceIndex(object):
                                    ds.ctypes.data, n.ctypes.data, _ptr(cnt)))
         return ids, ds, n, cnt
 
+    def search_served(self, query, k=10, epsilon=0.1, radius=-1.0, edge_size=-1, seed_mode=SEED_TREE):
+        """One query through the resident serving grid (serve.cpp); None when
+        the grid does not serve this index/request (ngt_amd_search_served = 1)."""
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(-1)
+        prm = SearchParams(k, epsilon, radius, edge_size, seed_mode, 0, 0, 0)
+        ids = np.zeros(k, np.uint32)
+        ds = np.zeros(k, np.float32)
+        n = ctypes.c_uint32()
+        cnt = np.zeros(COUNTERS, np.uint64)
+        rc = self.L.ngt_amd_search_served(self.h, byref(prm), q.ctypes.data, ids.ctypes.data, ds.ctypes.data,
+                                          byref(n), cnt.ctypes.data)
+        if rc == 1:
+            return None
+        _chk(rc)
+        return ids[:n.value], ds[:n.value], cnt
+
+    def serve_stop(self):
+        _chk(self.L.ngt_amd_serve_stop(self.h))
+
+    def serve_stats(self):
+        """(queries the serving grid answered, grids launched)."""
+        s, l = ctypes.c_uint64(), ctypes.c_uint64()
+        _chk(self.L.ngt_amd_serve_stats(self.h, byref(s), byref(l)))
+        return s.value, l.value
+
     def search_device(self, d_queries, query_bytes, nq, d_ids, d_dists, d_n, d_counters=None, k=10,
                       epsilon=0.1, radius=-1.0, edge_size=-1, seed_mode=SEED_TREE, d_seeds=None,
                       d_seed_off=None, stream=None, visited_hash_log2=0, distance_filter=0):

@@ -114,13 +114,15 @@ int main(int argc, char** argv) {
   FILE* o = fopen(argv[9], "wb");
   fwrite(g_ids, sizeof(uint32_t), total * g_k, o);
   fclose(o);
+  uint64_t batches = 0, served = 0;
+  ngt_get_coalesce_stats(g_index, &batches, &served, err);
   double sum = 0;
   for (size_t i = 0; i < total; i++) sum += g_lat[i];
   qsort(g_lat, total, sizeof(double), cmp_d);
   printf("{\"threads\": %d, \"calls\": %zu, \"wall_s\": %.6f, \"qps\": %.1f, \"latency_ms\": {\"mean\": %.4f, "
-         "\"p50\": %.4f, \"p99\": %.4f}}\n",
+         "\"p50\": %.4f, \"p99\": %.4f}, \"launches\": %llu, \"served\": %llu}\n",
          threads, total, wall, total / wall, 1e3 * sum / total, 1e3 * g_lat[total / 2],
-         1e3 * g_lat[(size_t)(0.99 * (total - 1))]);
+         1e3 * g_lat[(size_t)(0.99 * (total - 1))], (unsigned long long)batches, (unsigned long long)served);
   ngt_close_index(g_index);
   ngt_destroy_error_object(err);
   return 0;

@@ -1,0 +1,153 @@
+"""The resident serving grid (ngt_amd/csrc/serve.cpp, the SERVE form of
+search_lat.hip): single queries posted to a ring in pinned host memory and
+answered by a long-lived launch, the path concurrent ngt_search_index callers
+take (lib/NGT/Capi.cpp:377-406).  Bar: every served answer equals the oracle's
+restatement of NeighborhoodGraph::search (ids and float distance bits) and the
+batch launch's counters, for tree seeds (GraphAndTreeIndex::getSeedsFromTree
+on the device, Index.h:1524-1567) and random seeds (getRandomSeeds, the same
+rand() stream as a launch), under concurrency, with the HBM spill and slot
+reaping forced, and across a change of the index (the grid relaunches)."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from ngt_amd import lib
+from ngt_amd.device import SEED_RANDOM, SEED_TREE, DeviceIndex
+from test_gpu_lookahead import _graph
+
+pytestmark = pytest.mark.gpu
+
+
+def _anng(n=4000, dim=128, seed=3):
+    """A device-built ANNG + DVP tree over random float rows, loaded as a
+    search index (edge size for search 40, seed size 10)."""
+    rng = np.random.default_rng(seed)
+    rows = np.zeros((n, dim), np.float32)
+    rows[1:] = rng.random((n - 1, dim), dtype=np.float32)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    (offs, ids, _), tree = ix.build_anng(edge_size_for_creation=10, edge_size_for_search=40)
+    ix.set_graph(offs, ids)
+    ix.set_tree(tree)
+    ix.set_search_property(edge_size_for_search=40, seed_size=10)
+    return ix, rows, offs, ids, tree
+
+
+def _oracle(rows, offs, ids, tree, q, k, eps, es):
+    seeds, _, _ = O.tree_seeds("l2", tree, q, k, 10)
+    return O.search("l2", rows, offs, ids, q, seeds, k, np.float32(eps), edge_size=es)
+
+
+def test_served_equals_oracle_concurrent():
+    ix, rows, offs, ids, tree = _anng()
+    rng = np.random.default_rng(11)
+    qs = rng.random((96, rows.shape[1]), dtype=np.float32)
+    es = ix.resolve_edge_size(-1, 0.1)
+    s0, _ = ix.serve_stats()
+    got = [None] * len(qs)
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(t, len(qs), 8):
+                got[i] = ix.search_served(qs[i], k=10, epsilon=0.1, seed_mode=SEED_TREE)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]
+    s1, launches = ix.serve_stats()
+    assert s1 - s0 == len(qs) and launches >= 1
+    bi, bd, bn, bc = ix.search(qs, k=10, epsilon=0.1, seed_mode=SEED_TREE)
+    for i in range(len(qs)):
+        assert got[i] is not None, "the grid does not serve this index"
+        gi, gd, gc = got[i]
+        oi, od, _ = _oracle(rows, offs, ids, tree, qs[i], 10, 0.1, es)
+        assert list(gi) == list(oi), i
+        assert np.array_equal(gd.view(np.uint32), od.view(np.uint32)), i
+        for c in (0, 2, 4):  # distances, expansions, edges read: the launch's
+            assert gc[c] == bc[i, c], (i, c)
+    ix.close()
+
+
+@pytest.mark.parametrize("knobs", [{"NGT_AMD_LAT_TAIL": "128"}, {"NGT_AMD_LAT_SLOTS": "2"}])
+def test_served_spill_and_slots(monkeypatch, knobs):
+    """Long searches (k 30, epsilon 0.5, lists of 150) with the tail forced
+    small (HBM spill and refills) or two speculation slots (orphaned slots
+    reaped): answers equal the oracle's and the launch's counters."""
+    for kv in knobs.items():
+        monkeypatch.setenv(*kv)
+    n, dim, deg = 5000, 128, 150
+    rows, offs, edges = _graph(n, dim, deg, 91)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(4)
+    qs = rng.random((6, dim), dtype=np.float32)
+    for i, q in enumerate(qs):
+        lib().ngt_amd_srand(100 + i)
+        r = ix.search_served(q, k=30, epsilon=0.5, edge_size=0, seed_mode=SEED_RANDOM)
+        assert r is not None
+        lib().ngt_amd_srand(100 + i)
+        bi, bd, bn, bc = ix.search(q[None], k=30, epsilon=0.5, edge_size=0, seed_mode=SEED_RANDOM)
+        gi, gd, gc = r
+        assert list(gi) == list(bi[0, :bn[0]]), i
+        assert np.array_equal(gd.view(np.uint32), bd[0, :bn[0]].view(np.uint32)), i
+        assert gc[0] == bc[0, 0] and gc[2] == bc[0, 2], i
+    ix.close()
+
+
+def test_served_random_seeds_follow_the_rand_stream():
+    """getRandomSeeds draws the same rand() stream whether the query is served
+    or launched: after the same ngt_amd_srand both answer identically."""
+    n, dim, deg = 4000, 96, 24
+    rows, offs, edges = _graph(n, dim, deg, 12)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(8)
+    qs = rng.random((20, dim), dtype=np.float32)
+    lib().ngt_amd_srand(7)
+    served = [ix.search_served(q, k=10, epsilon=0.1, edge_size=0, seed_mode=SEED_RANDOM) for q in qs]
+    lib().ngt_amd_srand(7)
+    for i, q in enumerate(qs):
+        bi, bd, bn, _ = ix.search(q[None], k=10, epsilon=0.1, edge_size=0, seed_mode=SEED_RANDOM)
+        gi, gd, _ = served[i]
+        assert list(gi) == list(bi[0, :bn[0]]), i
+        assert np.array_equal(gd.view(np.uint32), bd[0, :bn[0]].view(np.uint32)), i
+    ix.close()
+
+
+def test_served_follows_index_changes():
+    """New rows under a running grid: the next query relaunches it over the
+    new index, and the grid stops on request and when idle."""
+    ix, rows, offs, ids, tree = _anng(n=3000, seed=5)
+    rng = np.random.default_rng(2)
+    q = rng.random(rows.shape[1], dtype=np.float32)
+    es = ix.resolve_edge_size(-1, 0.1)
+    gi, gd, _ = ix.search_served(q, k=10, epsilon=0.1)
+    oi, od, _ = _oracle(rows, offs, ids, tree, q, 10, 0.1, es)
+    assert list(gi) == list(oi)
+    _, l0 = ix.serve_stats()
+    rows2 = rows.copy()
+    rows2[1:] = rows2[1:] * np.float32(0.5) + np.float32(0.25)
+    ix.set_objects(rows2)
+    ix.set_graph(offs, ids)
+    ix.set_tree(tree)
+    gi, gd, _ = ix.search_served(q, k=10, epsilon=0.1)
+    oi, od, _ = _oracle(rows2, offs, ids, tree, q, 10, 0.1, es)
+    assert list(gi) == list(oi)
+    assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+    _, l1 = ix.serve_stats()
+    assert l1 > l0
+    ix.serve_stop()
+    gi2, _, _ = ix.search_served(q, k=10, epsilon=0.1)  # relaunched after the stop
+    assert list(gi2) == list(gi)
+    ix.close()
