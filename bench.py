@@ -1299,9 +1299,10 @@ def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):
 def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
     """tests/cxx/capi_threads.c compiled here with gcc against include/ and
     libngt_amd.so, run as a child process on the index directory: sequential
-    single-query latency and `threads` concurrent callers, for group-commit
-    the default two group-commit leaders (NGT_AMD_COALESCE_LEADERS), and
-    twice as many callers."""
+    single-query latency, `threads` concurrent callers and twice as many.
+    The calls are answered by the resident serving grid (serve.cpp; its grid
+    launches and answered calls are in each run's `launches` / `served`);
+    requests it does not take fall back to group-committed launches."""
     import subprocess
     exe = os.path.join(index_dir, "capi_threads")
     subprocess.check_call(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-o", exe,
@@ -1310,11 +1311,9 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
     qpath = os.path.join(index_dir, "queries.f32")
     np.ascontiguousarray(Q, np.float32).tofile(qpath)
     out = []
-    # (leader counts 4 and 8 measured slower than 2: 3.1k / 2.6k vs 5.4k QPS
-    # at 32 threads, profiles/r3/lat/capi.json)
-    for t, calls, leaders in [(1, 300, 2), (threads, 200, 2), (2 * threads, 150, 2)]:
+    for t, calls in [(1, 300), (threads, 200), (2 * threads, 150)]:
         ids_path = os.path.join(index_dir, "ids.u32")
-        env = dict(os.environ, NGT_AMD_COALESCE_LEADERS=str(leaders))
+        env = dict(os.environ)
         r = subprocess.run([exe, index_dir, qpath, str(Q.shape[0]), str(D), str(K), repr(float(eps)), str(t),
                             str(calls), ids_path], env=env, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
@@ -1325,10 +1324,10 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
         ids = np.fromfile(ids_path, np.uint32).reshape(-1, K).astype(np.int64)
         qi = np.arange(ids.shape[0]) % Q.shape[0]
         res["recall_at_10"] = recall_at(ids, gt[qi], K)
-        res["coalesce_leaders"] = leaders
         out.append(res)
-        log("C client: %d threads, leaders %d: %.0f QPS, latency mean %.3f ms p99 %.3f, recall %.4f" % (
-            t, leaders, res["qps"], res["latency_ms"]["mean"], res["latency_ms"]["p99"], res["recall_at_10"]))
+        log("C client: %d threads: %.0f QPS, latency mean %.3f ms p99 %.3f, recall %.4f (%d grid launches)" % (
+            t, res["qps"], res["latency_ms"]["mean"], res["latency_ms"]["p99"], res["recall_at_10"],
+            res.get("launches", -1)))
     return out
 
 

@@ -216,7 +216,8 @@ __device__ void serve_dispatch(const ServeArgs& sv) {
 // final.  Workers also leave on their own after life + idle + 1 s, so a grid
 // whose dispatcher block never got a CU still drains.
 __device__ bool serve_claim(const ServeArgs& sv, uint64_t t0, uint32_t& ticket) {
-  for (;;) {
+  // idle workers back off (all of them poll the same control line)
+  for (uint32_t idle = 0;; idle++) {
     uint32_t c = __hip_atomic_load(&sv.dctl->claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t av = __hip_atomic_load(&sv.dctl->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     if ((int32_t)(av - c) > 0) {
@@ -234,7 +235,9 @@ __device__ bool serve_claim(const ServeArgs& sv, uint64_t t0, uint32_t& ticket) 
       return false;
     }
     if (wall_clock64() - t0 > sv.life_ticks + sv.idle_ticks + 100000000ull) return false;
-    __builtin_amdgcn_s_sleep(4);
+    if (idle < 16) __builtin_amdgcn_s_sleep(2);
+    else if (idle < 256) __builtin_amdgcn_s_sleep(8);
+    else __builtin_amdgcn_s_sleep(32);
   }
 }
 

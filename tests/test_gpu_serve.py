@@ -65,7 +65,16 @@ def test_served_equals_oracle_concurrent():
     assert not errors, errors[:3]
     s1, launches = ix.serve_stats()
     assert s1 - s0 == len(qs) and launches >= 1
-    bi, bd, bn, bc = ix.search(qs, k=10, epsilon=0.1, seed_mode=SEED_TREE)
+    try:
+        bi, bd, bn, bc = ix.search(qs, k=10, epsilon=0.1, seed_mode=SEED_TREE)
+    except Exception as e:  # noqa: BLE001  (diagnostic: which form, and again?)
+        form = ix.last_search_lookahead()
+        try:
+            ix.search(qs, k=10, epsilon=0.1, seed_mode=SEED_TREE)
+            again = "ok"
+        except Exception as e2:  # noqa: BLE001
+            again = repr(e2)
+        raise AssertionError("batch search failed (form %d): %r; again: %s" % (form, e, again))
     for i in range(len(qs)):
         assert got[i] is not None, "the grid does not serve this index"
         gi, gd, gc = got[i]
