@@ -634,11 +634,20 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       SearchArgs b = a;
       b.lat_slots = cap <= 64 ? 32u : 16u;
       b.lat_tail = 4096u;
+      {
+        // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off
+        const int pool = [] {
+          const char* v = getenv("NGT_AMD_LAT_POOL");
+          return v ? std::max(0, std::min(32, atoi(v))) : 8;
+        }();
+        b.lat_pool = (uint32_t)std::max(0, std::min(pool, 64 - (int)b.lat_slots));
+      }
       while (search_lat_lds_bytes(b) > lds_max && b.lat_tail > 512u) b.lat_tail -= 256u;
       while (search_lat_lds_bytes(b) > lds_max && b.lat_slots > 8u) b.lat_slots -= 2u;
       // test knobs: a small tail forces the HBM spill, few slots the orphan path
       if (const char* v = getenv("NGT_AMD_LAT_TAIL")) b.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
       if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) b.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
+      b.lat_pool = std::min<uint32_t>(b.lat_pool, 64u - b.lat_slots);
       if (search_lat_lds_bytes(b) <= lds_max) {
         a = b;
         lat = true;

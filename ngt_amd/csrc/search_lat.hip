@@ -39,7 +39,7 @@ namespace ngt_amd {
 namespace {
 
 constexpr uint32_t kNoTag = 0xffu;  // head entry without a slot
-constexpr uint32_t kFree = 0u, kIssued = 1u, kReady = 3u;
+constexpr uint32_t kFree = 0u, kIssued = 1u, kPrep = 2u;
 
 struct LatCtl {
   uint32_t done;  // the commit wave has finished the query
@@ -49,7 +49,7 @@ struct LatCtl {
   float coef;
   float radius;
   uint32_t ns;    // serving form: seeds staged in the tail
-  uint32_t pad;
+  uint32_t expr;  // the commit wave's exploration radius (float bits), for the hop pool
   uint64_t sp[4]; // diagnostic build: speculation-wave cycles ([0] adjacency, [2] exact rows)
 };
 
@@ -60,11 +60,11 @@ struct LatSlot {
   uint64_t key;
   uint32_t state;
   uint32_t claim;
-  uint32_t done;
+  uint32_t pready; // parts finished (bit p: part p's entries and count are final)
   uint32_t deg;    // list length read (getEdgeSize cap), summed over the parts
   uint32_t gen;    // issue generation (the commit wave's)
   uint32_t pn[8];  // neighbours not yet visited when the part was read
-  uint32_t pad;
+  uint32_t owner;  // pool slots: 0 none, 1 the commit wave (adopted), 2 being recycled
 };
 
 struct LatLayout {
@@ -73,9 +73,10 @@ struct LatLayout {
   __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
   __host__ __device__ LatLayout(const SearchArgs& a, uint32_t cap, uint32_t waves) {
     uint32_t o = up16(sizeof(LatCtl));
-    off_slot = o; o = up16(o + sizeof(LatSlot) * a.lat_slots);
-    off_eid = o; o = up16(o + 4u * a.lat_slots * cap);
-    off_ed = o; o = up16(o + 4u * a.lat_slots * cap);
+    const uint32_t ns = a.lat_slots + a.lat_pool;
+    off_slot = o; o = up16(o + sizeof(LatSlot) * ns);
+    off_eid = o; o = up16(o + 4u * ns * cap);
+    off_ed = o; o = up16(o + 4u * ns * cap);
     off_tail = o; o = up16(o + 8u * a.lat_tail);
     off_q = o; o = up16(o + 4u * (uint32_t)a.dp);
     off_nid = o; o = up16(o + 256u);
@@ -306,6 +307,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
   const uint32_t cap = (uint32_t)(a.adj_stride < a.edge_size ? a.adj_stride : a.edge_size);
   constexpr uint32_t span = 32u;  // ids per part: one group of EG x 16 rows
   const uint32_t parts = (cap + span - 1u) / span;  // <= 8
+  const uint32_t pfull = (1u << parts) - 1u;        // every part finished
+  // the parts a commit pass reads: p and p + 1 (when there is one)
+  auto pmask = [&](uint32_t p) -> uint32_t { return pfull & (3u << p); };
   const LatLayout lay(a, cap, W);
   LatCtl* ctl = reinterpret_cast<LatCtl*>(smem);
   LatSlot* slots = reinterpret_cast<LatSlot*>(smem + lay.off_slot);
@@ -325,7 +329,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t NT = 64u * W;
   const uint32_t bm_words = (a.nrows + 31u) / 32u;
-  const uint32_t nslots = a.lat_slots;
+  const uint32_t nslots = a.lat_slots;  // the commit wave's slots
+  const uint32_t npool = a.lat_pool;    // then the hop pool: slots the speculation waves issue themselves
+  const uint32_t nall = nslots + npool;
   const uint32_t wg = blockIdx.x;
   uint64_t* spill = a.spill + (uint64_t)wg * a.spill_cap;
   const int g = lane & 3, rs = lane >> 2;
@@ -357,10 +363,12 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
                                                             : a.queries + (uint64_t)qi * a.query_bytes);
       uint4* d = reinterpret_cast<uint4*>(qlds);
       for (uint32_t i = tid; i < (uint32_t)a.dp / 4; i += NT) d[i] = s[i];
-      for (uint32_t i = tid; i < nslots; i += NT) {
+      for (uint32_t i = tid; i < nall; i += NT) {
         slots[i].state = kFree;
         slots[i].claim = 0u;
         slots[i].gen = 0u;
+        slots[i].owner = 0u;
+        slots[i].pready = 0u;
       }
       if (tid == 0) {
         ctl->done = 0u;
@@ -402,7 +410,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if ((uint32_t)lane == pos) rk = key;
         nres = nres + 1 < k ? nres + 1 : k;
       };
-      uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0;
+      uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0, nadopt = 0;
+      (void)nadopt;
       (void)nwait;
       // diagnostic build only: shader-clock totals per phase
       uint64_t t_pop = 0, t_wait = 0, t_list = 0, t_feed = 0, t_last = 0;
@@ -410,6 +419,12 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       float radius = radq;
       uint32_t qerr = 0;  // the batch kernel's error bits, this query's
       float expr = 0.f;
+      // expr, published for the speculation waves' hop choices
+      auto set_expr = [&]() {
+        expr = __fmul_rn(coefq, radius);
+        if (lane == 0)
+          __hip_atomic_store(&ctl->expr, __float_as_uint(expr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
       // unchecked set: head (registers, sorted, hn keys) < B <= tail (LDS,
       // ntail keys) < T <= spill (HBM, nspill keys)
       uint64_t hk = ~0ull;
@@ -615,16 +630,55 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         hn--;
         return true;
       };
+      // a slot the commit wave is done with: its own slots back to freem, pool
+      // slots back to the pool (unowned, free)
+      auto release_slot = [&](uint32_t t) {
+        if (t < nslots) {
+          if (lane == 0) slots[t].state = kFree;
+          freem |= 1ull << t;
+        } else if (lane == 0) {
+          // free before unowned: an unowned issued slot could be taken for a
+          // recycle while a speculation wave still works on it
+          lds_store_rel(&slots[t].state, kFree);
+          lds_store_rel(&slots[t].owner, 0u);
+        }
+      };
+      // a pool slot the speculation waves issued for this key: owned by the
+      // commit wave from here on (CAS on the owner word; the key is re-read
+      // after it, since a recycle may have re-keyed the slot meanwhile)
+      auto adopt = [&](uint64_t key) -> uint32_t {
+        if (npool == 0) return kNoTag;
+        const uint32_t pl = nslots + (uint32_t)lane;
+        const bool c = (uint32_t)lane < npool && lds_load_acq(&slots[pl].state) == kIssued &&
+                       slots[pl].owner == 0u && slots[pl].key == key;
+        uint64_t cm = ballot64(c);
+        while (cm) {
+          const uint32_t t = nslots + (uint32_t)(__ffsll((long long)cm) - 1);
+          cm &= cm - 1;
+          uint32_t ok = 0;
+          if (lane == 0) {
+            uint32_t e = 0u;
+            ok = __hip_atomic_compare_exchange_strong(&slots[t].owner, &e, 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+          }
+          if (!__builtin_amdgcn_readfirstlane((int)ok)) continue;
+          if (lds_load_acq(&slots[t].state) == kIssued && slots[t].key == key) {
+            nadopt++;
+            return t;
+          }
+          if (lane == 0) lds_store_rel(&slots[t].owner, 0u);
+        }
+        return kNoTag;
+      };
       // free the orphaned slots whose speculation has finished
       auto reap = [&]() {
         uint64_t o = orphan;
         while (o) {
           const int s = __ffsll((long long)o) - 1;
           o &= o - 1;
-          if (lds_load_acq(&slots[s].state) == kReady) {
-            if (lane == 0) slots[s].state = kFree;
+          if (lds_load_acq(&slots[s].pready) == pfull) {
+            release_slot((uint32_t)s);
             orphan &= ~(1ull << s);
-            freem |= 1ull << s;
           }
         }
       };
@@ -650,7 +704,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
           slots[s].key = key;
-          slots[s].done = 0u;
+          slots[s].pready = 0u;
           slots[s].deg = 0u;
           slots[s].gen = gen;
         }
@@ -668,9 +722,13 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         while (need) {
           const int l = __ffsll((long long)need) - 1;
           need &= need - 1;
-          if (freem == 0ull) break;
-          const uint32_t s = issue(readlane_u64(hk, l));
-          if (stuck) break;
+          const uint64_t key = readlane_u64(hk, l);
+          uint32_t s = adopt(key);
+          if (s == kNoTag) {
+            if (freem == 0ull) break;
+            s = issue(key);
+            if (stuck) break;
+          }
           if (lane == l) ht = s;
         }
       };
@@ -702,7 +760,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           res_push(key);
           if (nres >= k) {
             radius = key_dist(readlane_u64(rk, (int)k - 1));
-            expr = __fmul_rn(coefq, radius);
+            set_expr();
           }
           __builtin_amdgcn_wave_barrier();
           okmask &= ~((2ull << j) - 1ull);
@@ -723,7 +781,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
         sp = a.seeds;
       }
-      expr = __fmul_rn(coefq, radius);
+      set_expr();
       for (uint32_t base = 0; base < ns; base += 64) {
         const uint32_t m = ns - base < 64 ? (uint32_t)(ns - base) : 64u;
         if ((uint32_t)lane < m) nid[lane] = sp[sb + base + lane];
@@ -745,7 +803,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       }
       ndist = ns;
       if (nres >= k) radius = key_dist(readlane_u64(rk, (int)k - 1));
-      expr = __fmul_rn(coefq, radius);
+      set_expr();
       feed();
 
       // ---- best-first loop (Graph.cpp:430-486) ------------------------------
@@ -758,26 +816,22 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (!pop(key, tag)) break;
         if (key_dist(key) > expr) break;  // Graph.cpp:433-435
         if (tag == kNoTag) {
-          tag = issue(key);
-          nwait++;
+          tag = adopt(key);
+          if (tag == kNoTag) {
+            tag = issue(key);
+            nwait++;
+          }
         }
         if (stuck) break;
         NGT_MARK(t_pop);
         feed();  // keep the speculation ahead while this node's list lands
         NGT_MARK(t_feed);
-        if (lds_load_acq(&slots[tag].state) != kReady) nstall++;
-        for (uint32_t spin = 0; lds_load_acq(&slots[tag].state) != kReady; spin++) {
-          if (spin > (1u << 24)) {
-            qerr |= 16u;
-            stuck = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (stuck) break;
+        // each pass waits only for its own two parts: the first parts of a
+        // list are applied (and their accepts handed out) while the later
+        // ones are still in flight
+        if ((lds_load_acq(&slots[tag].pready) & pmask(0u)) != pmask(0u)) nstall++;
         NGT_MARK(t_wait);
         nexp++;
-        nedge += slots[tag].deg;
         // the parts of the list in order, two per pass (lanes 0-31 part p,
         // 32-63 part p+1; each part compacted in list order, so lane order
         // is neighbour order): visited test, mark, then the accepts in
@@ -791,6 +845,15 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           const uint32_t half = (uint32_t)lane >> 5, sub = (uint32_t)lane & 31u;
 #pragma unroll 1
           for (uint32_t p = 0; p < parts; p += 2) {
+            for (uint32_t spin = 0; (lds_load_acq(&slots[tag].pready) & pmask(p)) != pmask(p); spin++) {
+              if (spin > (1u << 24)) {
+                qerr |= 16u;
+                stuck = true;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if (stuck) break;
             const uint32_t pp = p + half;
             const uint32_t np = pp < parts ? slots[tag].pn[pp] : 0u;
             const bool in = sub < np;
@@ -808,8 +871,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
             }
           }
         }
-        if (lane == 0) slots[tag].state = kFree;
-        freem |= 1ull << tag;
+        if (stuck) break;
+        nedge += slots[tag].deg;
+        release_slot(tag);
         NGT_MARK(t_list);
         feed();
         NGT_MARK(t_feed);
@@ -868,11 +932,71 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       }
     } else {
       // =================== speculation waves =================================
+      // issue a pool slot for `key` unless some slot already speculates it:
+      // a free pool slot, else recycle the finished unowned one with the
+      // largest key (when that key is larger than this one)
+      auto hop_issue = [&](uint64_t key) {
+        const bool dup = (uint32_t)lane < nall && slots[lane].key == key && lds_load_acq(&slots[lane].state) == kIssued;
+        if (ballot64(dup)) return;
+        const uint32_t pl = nslots + (uint32_t)lane;
+        const uint32_t pst = (uint32_t)lane < npool ? lds_load_acq(&slots[pl].state) : 0xffu;
+        uint32_t t = ~0u;
+        bool fresh_slot = false;
+        uint64_t fm = ballot64(pst == kFree);
+        while (fm && t == ~0u) {
+          const uint32_t c = nslots + (uint32_t)(__ffsll((long long)fm) - 1);
+          fm &= fm - 1;
+          uint32_t ok = 0;
+          if (lane == 0) {
+            uint32_t e = kFree;
+            ok = __hip_atomic_compare_exchange_strong(&slots[c].state, &e, kPrep, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+          }
+          if (__builtin_amdgcn_readfirstlane((int)ok)) {
+            t = c;
+            fresh_slot = true;
+          }
+        }
+        if (t == ~0u) {
+          const bool rc = pst == kIssued && slots[pl].owner == 0u && lds_load_acq(&slots[pl].pready) == pfull;
+          const uint64_t rk2 = rc ? slots[pl].key : 0ull;
+          const uint64_t worst = uniform_u64_lat(~wave_min_u64(~rk2));
+          if (worst <= key) return;  // every finished slot is a better bet
+          const uint32_t c = nslots + (uint32_t)(__ffsll((long long)ballot64(rc && rk2 == worst)) - 1);
+          uint32_t ok = 0;
+          if (lane == 0) {
+            uint32_t e = 0u;
+            ok = __hip_atomic_compare_exchange_strong(&slots[c].owner, &e, 2u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+          }
+          if (!__builtin_amdgcn_readfirstlane((int)ok)) return;
+          // still finished and issued under the lock (only a free slot changes state otherwise)
+          if (lds_load_acq(&slots[c].state) != kIssued || lds_load_acq(&slots[c].pready) != pfull) {
+            if (lane == 0) lds_store_rel(&slots[c].owner, 0u);
+            return;
+          }
+          t = c;
+        }
+        const uint32_t gen = (slots[t].gen + 1u) & 0xffffffu;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          slots[t].key = key;
+          slots[t].pready = 0u;
+          slots[t].deg = 0u;
+          slots[t].gen = gen;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          lds_store_rel(&slots[t].claim, gen << 8);
+          lds_store_rel(&slots[t].owner, 0u);
+          if (fresh_slot) lds_store_rel(&slots[t].state, kIssued);
+        }
+      };
       for (;;) {
         if (lds_load_acq(&ctl->done)) break;
         // the issued slot with the smallest key
-        const uint32_t st = (uint32_t)lane < nslots ? lds_load_acq(&slots[lane].state) : kFree;
-        const uint32_t cw = (uint32_t)lane < nslots ? lds_load_acq(&slots[lane].claim) : 0u;
+        const uint32_t st = (uint32_t)lane < nall ? lds_load_acq(&slots[lane].state) : kFree;
+        const uint32_t cw = (uint32_t)lane < nall ? lds_load_acq(&slots[lane].claim) : 0u;
         const uint64_t cand = st == kIssued && (cw & 0xffu) < parts ? slots[lane].key : ~0ull;
         const uint64_t m = uniform_u64_lat(wave_min_u64(cand));
         if (m == ~0ull) {
@@ -919,25 +1043,39 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         // the comparator's exact distances of those neighbours
         // (PrimitiveComparator::compareL2 through l2_fold_rows): a quad per
         // row, EG groups of 16 rows in flight
+        // the smallest key among them within the exploration radius: the
+        // neighbour the commit wave most likely accepts and pops soon (hop)
+        uint64_t hop = ~0ull;
         {
           const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
           for (uint32_t r0 = 0; r0 < np; r0 += 16u * EG) {
             float4 v[EG][NCH];
+            uint32_t rid[EG];
 #pragma unroll
             for (int j = 0; j < EG; j++) {
+              rid[j] = 0u;
               if (r0 + 16u * j >= np) continue;
               const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
-              const uint32_t rid = rr < np ? sid[rr] : 0u;
-              const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)rid * a.row_bytes) + g;
+              rid[j] = rr < np ? sid[rr] : 0u;
+              const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)rid[j] * a.row_bytes) + g;
 #pragma unroll
               for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
             }
+            const float ex = npool ? __uint_as_float(__hip_atomic_load(&ctl->expr, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_WORKGROUP))
+                                   : 0.f;
 #pragma unroll
             for (int j = 0; j < EG; j++) {
               if (r0 + 16u * j >= np) continue;
               const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
               const float d = l2_fold_rows<NCH>(qq, v[j]);
-              if (g == 0 && rr < np) sd[rr] = d;
+              if (g == 0 && rr < np) {
+                sd[rr] = d;
+                if (d <= ex) {
+                  const uint64_t kk = make_key(d, rid[j]);
+                  hop = kk < hop ? kk : hop;
+                }
+              }
             }
           }
         }
@@ -950,11 +1088,14 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           atomicAdd(&slots[sl].deg, live);
         }
         __builtin_amdgcn_wave_barrier();
-        uint32_t prev = 0;
+        // the part's bit is this wave's last touch of the slot: once every
+        // bit is set, the commit wave may free and reissue it
         if (lane == 0)
-          prev = __hip_atomic_fetch_add(&slots[sl].done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
-        if (prev + 1u == parts && lane == 0) lds_store_rel(&slots[sl].state, kReady);  // the last part completes it
+          __hip_atomic_fetch_or(&slots[sl].pready, 1u << part, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (npool) {
+          hop = uniform_u64_lat(wave_min_u64(hop));
+          if (hop != ~0ull) hop_issue(hop);
+        }
       }
     }
     __syncthreads();

@@ -62,7 +62,7 @@ struct ServeConfig {
   const void* pivot;
   const void* leaf_ids;
   uint64_t nrows, adj_stride, es, rows_version, adj_version, tree_version;
-  int32_t use_tree, all_leaf, seed_size, lat_slots, lat_tail, pad;
+  int32_t use_tree, all_leaf, seed_size, lat_slots, lat_tail, lat_pool;
   bool operator==(const ServeConfig& o) const { return memcmp(this, &o, sizeof o) == 0; }
 };
 
@@ -248,10 +248,19 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   const size_t lds_max = std::max<size_t>(64 * 1024, std::min<size_t>(ix->lds_per_block, ix->lds_per_cu));
   a.lat_slots = cap <= 64 ? 32u : 16u;
   a.lat_tail = 4096u;
+  {
+    // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off
+    const int pool = [] {
+      const char* v = getenv("NGT_AMD_LAT_POOL");
+      return v ? std::max(0, std::min(32, atoi(v))) : 8;
+    }();
+    a.lat_pool = (uint32_t)std::max(0, std::min(pool, 64 - (int)a.lat_slots));
+  }
   while (search_lat_lds_bytes(a) > lds_max && a.lat_tail > 512u) a.lat_tail -= 256u;
   while (search_lat_lds_bytes(a) > lds_max && a.lat_slots > 8u) a.lat_slots -= 2u;
   if (const char* v = getenv("NGT_AMD_LAT_TAIL")) a.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
   if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) a.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
+  a.lat_pool = std::min<uint32_t>(a.lat_pool, 64u - a.lat_slots);
   if (search_lat_lds_bytes(a) > lds_max) return 1;
   cfg = ServeConfig{};
   cfg.rows = ix->rows.p;
@@ -269,6 +278,7 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   cfg.seed_size = tree ? std::max(ix->seed_size, 0) : 0;
   cfg.lat_slots = (int32_t)a.lat_slots;
   cfg.lat_tail = (int32_t)a.lat_tail;
+  cfg.lat_pool = (int32_t)a.lat_pool;
   return 0;
 }
 
