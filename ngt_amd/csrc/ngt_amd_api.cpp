@@ -635,10 +635,12 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       b.lat_slots = cap <= 64 ? 32u : 16u;
       b.lat_tail = 4096u;
       {
-        // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off
+        // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off (the
+        // default: with 8 slots a served C1 ANNG search timed out waiting for a
+        // slot, error 16 -- tests/test_cxx_api.py, profiles/r3w)
         const int pool = [] {
           const char* v = getenv("NGT_AMD_LAT_POOL");
-          return v ? std::max(0, std::min(32, atoi(v))) : 8;
+          return v ? std::max(0, std::min(32, atoi(v))) : 0;
         }();
         b.lat_pool = (uint32_t)std::max(0, std::min(pool, 64 - (int)b.lat_slots));
       }

@@ -249,10 +249,11 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   a.lat_slots = cap <= 64 ? 32u : 16u;
   a.lat_tail = 4096u;
   {
-    // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off
+    // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off (the
+    // default; see ngt_amd_api.cpp)
     const int pool = [] {
       const char* v = getenv("NGT_AMD_LAT_POOL");
-      return v ? std::max(0, std::min(32, atoi(v))) : 8;
+      return v ? std::max(0, std::min(32, atoi(v))) : 0;
     }();
     a.lat_pool = (uint32_t)std::max(0, std::min(pool, 64 - (int)a.lat_slots));
   }
