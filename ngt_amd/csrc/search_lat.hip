@@ -687,7 +687,21 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       // every wait below is bounded: a slot that never becomes ready (never
       // expected) flags error 16 and ends the query instead of hanging the CU
       bool stuck = false;
+      const uint64_t ownm = nslots >= 64 ? ~0ull : ((1ull << nslots) - 1ull);  // the commit wave's own slots
       auto issue = [&](uint64_t key) -> uint32_t {
+        if (freem == 0ull && (orphan & ownm) == 0ull) {
+          // every own slot is held by a head entry: the node just released was
+          // a pool slot, which goes back to the pool, so nothing comes back to
+          // freem by itself -- the deepest head entry holding an own slot
+          // gives it up (orphaned, freed once its speculation is done)
+          const uint64_t om = ballot64(ht < nslots);
+          if (om != 0ull) {
+            const int l = 63 - __builtin_clzll(om);
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)ht, l);
+            if (lane == l) ht = kNoTag;
+            orphan |= 1ull << t;
+          }
+        }
         for (uint32_t spin = 0; freem == 0ull; spin++) {
           reap();
           if (freem != 0ull) break;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # error 16 in the served latency kernel (test_cxx_search_matches_reference on
-# the C1 ANNG): hop pool default (8) vs off; then, with the pool off, the whole
+# the C1 ANNG, hop pool of 8): pool 8 with the own-slot steal vs off; then, with the pool off, the whole
 # GPU suite, smoke, the C2 bench and the C-API line
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r3w
@@ -20,4 +20,7 @@ python3 -c "import json; d=json.load(open('gpurun_out/r3w/bench_c2.json')); prin
 timeout -k 10 400 python -u bench.py --mode capi --no-cpu --eps 0.0703125 \
   > gpurun_out/r3w/capi.json 2> gpurun_out/r3w/capi.log || { tail -5 gpurun_out/r3w/capi.log; exit 1; }
 grep -h "C client" gpurun_out/r3w/capi.log
+# the pool with the own-slot steal: lookahead/latency and serving tests at 8 slots
+NGT_AMD_LAT_POOL=8 $T tests/test_gpu_lookahead.py tests/test_gpu_serve.py tests/test_gpu_api.py > gpurun_out/r3w/la_p8.log 2>&1
+echo "lookahead/serve/api pool 8 rc=$? $(tail -1 gpurun_out/r3w/la_p8.log)"
 exit 0
