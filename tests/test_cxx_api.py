@@ -81,7 +81,15 @@ def test_sample_compiles_and_reads_accuracy_table(sample):
 
 
 @pytest.mark.gpu
-def test_cxx_search_matches_reference(sample):
+@pytest.mark.parametrize("pool", [None, "8"])
+def test_cxx_search_matches_reference(sample, monkeypatch, pool):
+    """Single-query searches through the C++ facade (the serving grid of the
+    latency kernel), also with an 8-slot hop pool: with it, every own slot
+    could end up held by head entries while a popped pool slot went back to
+    the pool -- the commit wave then waited for a slot forever (error 16)
+    until the deepest holder gave its slot up."""
+    if pool is not None:
+        monkeypatch.setenv("NGT_AMD_LAT_POOL", pool)
     exe, qf, d = sample
     ids, ds, nd, first = parse(run(exe, "search", os.path.join(GOLD, "c1_anng"), qf, 10, 0.1), 100, 10)
     g = np.load(os.path.join(GOLD, "search_c1_anng_tw_0.1.npz"))
