@@ -93,6 +93,7 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
   if (prm->edge_size_for_creation <= 0 || prm->batch_size_for_creation <= 0)
     return fail("ngt_amd_build_begin: edge_size_for_creation and batch_size_for_creation must be > 0");
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   delete ix->build;
   auto* b = new BuildState();
   ix->build = b;
@@ -132,13 +133,10 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
 extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64_t end_id) {
   if (!ix || !ix->build) return fail("ngt_amd_build_insert: call ngt_amd_build_begin first");
   HIP_OK(hipSetDevice(ix->device));
-  // the insertion searches must not build copies derived from the adjacency
-  // this call keeps changing
-  struct Building {
-    ngt_amd_index* ix;
-    ~Building() { ix->building = false; }
-  } building_guard{ix};
-  ix->building = true;
+  serve_quiesce(ix);
+  // the insertion searches never rebuild the padded adjacency this call keeps
+  // changing: build_begin set max_degree = adj_stride, so the copy always
+  // holds every edge they read
   BuildState& b = *ix->build;
   hipStream_t s = ix->stream;
   const uint64_t rb = ix->row_bytes;
@@ -439,6 +437,7 @@ extern "C" int ngt_amd_build_set_graph(ngt_amd_index* ix, const uint64_t* offset
   if (!ix || !ix->build || !offsets || graph_rows > ix->nrows) return fail("ngt_amd_build_set_graph: bad arguments");
   if (offsets[graph_rows] && (!ids || !dists)) return fail("ngt_amd_build_set_graph: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   BuildState& b = *ix->build;
   const uint64_t S = b.adj_stride;
   std::vector<uint32_t> adj((size_t)ix->nrows * S, 0u);

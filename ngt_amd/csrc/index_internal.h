@@ -217,7 +217,6 @@ struct ngt_amd_index {
   uint64_t adj_stride = 0;
   uint64_t max_degree = 0;       // widest adjacency list
   uint64_t adj_version = 0;      // bumped whenever adj changes
-  bool building = false;         // ANNG construction in progress (adj changes per batch)
 
   bool has_graph = false;
   std::vector<uint8_t> h_graph_empty;
@@ -265,6 +264,10 @@ SearchCtx* ctx_for(ngt_amd_index* ix, hipStream_t s);
 int ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds_per_slot, uint32_t nq, hipStream_t s);
 // device error flag of stream s's launches: read (synchronising s), clear, return
 int take_device_error(ngt_amd_index* ix, hipStream_t s, int* flag);
+// zero stream s's error word, ordered on s (the start of a host-API call)
+int clear_device_error(ngt_amd_index* ix, hipStream_t s);
+// the names of the bits set in a device error word ("1: ...; 32: ...")
+std::string device_error_text(int flag);
 // host-API call contexts (own stream + persistent buffers), pooled per index
 CallCtx* acquire_call(ngt_amd_index* ix);
 void release_call(ngt_amd_index* ix, CallCtx* c);
@@ -285,6 +288,9 @@ int build_padded_adjacency(ngt_amd_index* ix, uint64_t need);
 uint64_t adjacency_need(const ngt_amd_index* ix, uint64_t es);
 // stop and free the serving grid (serve.cpp); no-op without one
 void serve_destroy(ngt_amd_index* ix);
+// stop the serving grid before the index's buffers change (waits for the
+// served calls in flight; new ones take the launch path meanwhile)
+void serve_quiesce(ngt_amd_index* ix);
 // GraphIndex::getRandomSeeds (Index.h:775-801) over the library's rand() stream
 // (a fresh process's glibc sequence, ngt_amd_srand)
 std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off);

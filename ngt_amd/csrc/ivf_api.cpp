@@ -178,6 +178,7 @@ extern "C" int ngt_amd_ngtq_search(ngt_amd_index* ix, const ngt_amd_ngtq_search_
   CallCtx* cc = g.c;
   if (!cc) return -1;
   hipStream_t s = cc->stream;
+  if (clear_device_error(ix, s)) return -1;
   if (upload_queries(ix, queries, nq, cc->raw, cc->prep, s)) return -1;
   HIP_OK(cc->ids.alloc((size_t)nq * prm->size));
   HIP_OK(cc->dists.alloc((size_t)nq * prm->size));
@@ -189,7 +190,7 @@ extern "C" int ngt_amd_ngtq_search(ngt_amd_index* ix, const ngt_amd_ngtq_search_
   HIP_OK(hipMemcpyAsync(n, cc->n.p, (size_t)nq * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   int flag = 0;
   if (take_device_error(ix, s, &flag)) return -1;
-  if (flag) return fail("ngt_amd_ngtq_search: device error flag %d", flag);
+  if (flag) return fail("ngt_amd_ngtq_search: device error flag %d (%s)", flag, device_error_text(flag).c_str());
   return 0;
 }
 

@@ -107,6 +107,7 @@ extern "C" int ngt_amd_index_set_objects(ngt_amd_index* ix, const void* rows, ui
                                          const uint8_t* valid) {
   if (!ix || !rows || nrows == 0) return fail("ngt_amd_index_set_objects: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   HIP_OK(ix->rows.upload(static_cast<const uint8_t*>(rows), nrows * ix->row_bytes));
   ix->nrows = nrows;
   ix->rows_version++;
@@ -120,6 +121,7 @@ extern "C" int ngt_amd_index_set_objects(ngt_amd_index* ix, const void* rows, ui
 extern "C" int ngt_amd_index_set_objects_device(ngt_amd_index* ix, const void* d_rows, uint64_t nrows) {
   if (!ix || !d_rows || nrows == 0) return fail("ngt_amd_index_set_objects_device: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   ix->rows.release();
   ix->rows.p = (uint8_t*)d_rows;
   ix->rows.n = nrows * ix->row_bytes;
@@ -150,6 +152,7 @@ int ngt_amd::build_padded_adjacency(ngt_amd_index* ix, uint64_t need) {
   if (need == 0 || need > 256) return 0;
   if (ix->adj.p && ix->adj_stride >= need) return 0;
   const uint64_t stride = (need + 15) & ~15ull;
+  serve_quiesce(ix);  // a running grid reads the copy being replaced
   ix->adj.release();
   ix->adj_stride = 0;
   HIP_OK(ix->adj.alloc(ix->nrows * stride));
@@ -172,6 +175,7 @@ uint64_t ngt_amd::adjacency_need(const ngt_amd_index* ix, uint64_t es) {
 }
 
 static int reset_adjacency(ngt_amd_index* ix, const uint64_t* h_offsets) {
+  serve_quiesce(ix);
   ix->max_degree = max_degree_of(h_offsets, ix->nrows);
   ix->adj.release();
   ix->adj_stride = 0;
@@ -191,6 +195,7 @@ extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offset
     if (edges[i] == 0 || edges[i] >= ix->nrows)
       return fail("ngt_amd_index_set_graph: edge %llu -> %u out of range", (unsigned long long)i, edges[i]);
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   HIP_OK(ix->edge_off.upload(offsets, ix->nrows + 1));
   HIP_OK(ix->edges.upload(edges, nedges));
   ix->nedges = nedges;
@@ -203,6 +208,7 @@ extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t*
                                               const uint32_t* d_edges, uint64_t nedges) {
   if (!ix || !d_offsets) return fail("ngt_amd_index_set_graph_device: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   ix->edge_off.release();
   ix->edges.release();
   ix->edge_off.p = const_cast<uint64_t*>(d_offsets);
@@ -223,6 +229,7 @@ extern "C" int ngt_amd_index_set_tree(ngt_amd_index* ix, const void* in_pivot, u
                                       uint32_t n_leaf, const uint32_t* leaf_ids, uint64_t n_leaf_ids) {
   if (!ix || children < 2 || !leaf_off) return fail("ngt_amd_index_set_tree: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
+  serve_quiesce(ix);
   HIP_OK(ix->in_pivot.upload(static_cast<const uint8_t*>(in_pivot), (size_t)n_internal * ix->row_bytes));
   HIP_OK(ix->in_child.upload(in_child, (size_t)n_internal * children));
   HIP_OK(ix->in_border.upload(in_border, (size_t)n_internal * (children - 1)));
@@ -280,9 +287,14 @@ ngt_amd::SearchCtx* ngt_amd::ctx_for(ngt_amd_index* ix, hipStream_t s) {
     }
   auto* c = new SearchCtx();
   c->stream = s;
+  // the error word is zeroed on s itself and waited for: a null-stream
+  // hipMemset is not ordered with a non-blocking stream, and recycled device
+  // memory may hold anything until it lands (GPUTEST_r03's flag 36: a fresh
+  // call stream read a stale word while the null stream's fill sat behind the
+  // resident serving grid)
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       c->work.alloc(4) != hipSuccess || c->err.alloc(1) != hipSuccess ||
-      hipMemset(c->err.p, 0, sizeof(int)) != hipSuccess) {
+      hipMemsetAsync(c->err.p, 0, sizeof(int), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     delete c;
     fail("search: cannot create the launch context of stream %p", (void*)s);
     return nullptr;
@@ -290,6 +302,37 @@ ngt_amd::SearchCtx* ngt_amd::ctx_for(ngt_amd_index* ix, hipStream_t s) {
   ix->ctxs.push_back(c);
   ix->last_ctx = c;
   return c;
+}
+
+int ngt_amd::clear_device_error(ngt_amd_index* ix, hipStream_t s) {
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
+  HIP_OK(hipMemsetAsync(c->err.p, 0, sizeof(int), s));
+  return 0;
+}
+
+// The bits the device code sets in a launch context's error word.
+std::string ngt_amd::device_error_text(int flag) {
+  static const char* names[] = {
+      "unchecked-set spill capacity exceeded (result list truncated)",        // 1: every search kernel
+      "zero-norm query under a normalized metric",                            // 2: prep_kernels.hip
+      "one-expansion kernel: stale chunk minimum (invariant)",                // 4: search_kernels.hip
+      "lookahead kernel: selection target exceeded by equal keys (invariant)",  // 8: search_la.hip
+      "latency kernel: a speculation slot never became ready (timeout)",      // 16: search_lat.hip
+      "latency kernel: tail-to-spill threshold selection check",              // 32
+      "latency kernel: spill refill selection check",                         // 64
+      "latency kernel: head refill selection check",                          // 128
+  };
+  std::string out;
+  for (int b = 0; b < 31; b++) {
+    if (!(flag & (1 << b))) continue;
+    if (!out.empty()) out += "; ";
+    char num[16];
+    snprintf(num, sizeof num, "%d: ", 1 << b);
+    out += num;
+    out += b < 8 ? names[b] : "unknown bit";
+  }
+  return out;
 }
 
 int ngt_amd::take_device_error(ngt_amd_index* ix, hipStream_t s, int* flag) {
@@ -634,22 +677,11 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       SearchArgs b = a;
       b.lat_slots = cap <= 64 ? 32u : 16u;
       b.lat_tail = 4096u;
-      {
-        // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off (the
-        // default: with 8 slots a served C1 ANNG search timed out waiting for a
-        // slot, error 16 -- tests/test_cxx_api.py, profiles/r3w)
-        const int pool = [] {
-          const char* v = getenv("NGT_AMD_LAT_POOL");
-          return v ? std::max(0, std::min(32, atoi(v))) : 0;
-        }();
-        b.lat_pool = (uint32_t)std::max(0, std::min(pool, 64 - (int)b.lat_slots));
-      }
       while (search_lat_lds_bytes(b) > lds_max && b.lat_tail > 512u) b.lat_tail -= 256u;
       while (search_lat_lds_bytes(b) > lds_max && b.lat_slots > 8u) b.lat_slots -= 2u;
       // test knobs: a small tail forces the HBM spill, few slots the orphan path
       if (const char* v = getenv("NGT_AMD_LAT_TAIL")) b.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
       if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) b.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
-      b.lat_pool = std::min<uint32_t>(b.lat_pool, 64u - b.lat_slots);
       if (search_lat_lds_bytes(b) <= lds_max) {
         a = b;
         lat = true;
@@ -843,6 +875,9 @@ extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* pr
   CallCtx* cc = g.c;
   if (!cc) return -1;
   hipStream_t s = cc->stream;
+  // this call's error word starts clear on its own stream: a flag names the
+  // launches of this call and nothing earlier
+  if (clear_device_error(ix, s)) return -1;
   if (upload_queries(ix, queries, nq, cc->raw, cc->prep, s)) return -1;
   HIP_OK(cc->ids.alloc((size_t)nq * prm->k));
   HIP_OK(cc->dists.alloc((size_t)nq * prm->k));
@@ -869,7 +904,7 @@ extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* pr
                           hipMemcpyDeviceToHost, s));
   int herr = 0;
   if (take_device_error(ix, s, &herr)) return -1;
-  if (herr) return fail("ngt_amd_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
+  if (herr) return fail("ngt_amd_search: device error flag %d (%s)", herr, device_error_text(herr).c_str());
   return 0;
 }
 

@@ -95,7 +95,6 @@ struct SearchArgs {
   // latency kernel (search_lat.hip): speculation slots and LDS tail keys
   uint32_t lat_slots;
   uint32_t lat_tail;
-  uint32_t lat_pool;             // hop pool: slots the speculation waves issue (0 = none)
 };
 
 // Serving form of the latency kernel (search_lat.hip, serve.cpp): a resident

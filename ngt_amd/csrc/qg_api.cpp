@@ -423,6 +423,7 @@ extern "C" int ngt_amd_qg_search(ngt_amd_index* ix, const ngt_amd_qg_search_para
   CallCtx* cc = g.c;
   if (!cc) return -1;
   hipStream_t s = cc->stream;
+  if (clear_device_error(ix, s)) return -1;
   if (upload_queries(ix, queries, nq, cc->raw, cc->prep, s)) return -1;
   HIP_OK(cc->ids.alloc((size_t)nq * prm->k));
   HIP_OK(cc->dists.alloc((size_t)nq * prm->k));
@@ -449,6 +450,6 @@ extern "C" int ngt_amd_qg_search(ngt_amd_index* ix, const ngt_amd_qg_search_para
                           hipMemcpyDeviceToHost, s));
   int herr = 0;
   if (take_device_error(ix, s, &herr)) return -1;
-  if (herr) return fail("ngt_amd_qg_search: device error flag %d (unchecked-set spill capacity exceeded)", herr);
+  if (herr) return fail("ngt_amd_qg_search: device error flag %d (%s)", herr, device_error_text(herr).c_str());
   return 0;
 }

@@ -39,7 +39,7 @@ namespace ngt_amd {
 namespace {
 
 constexpr uint32_t kNoTag = 0xffu;  // head entry without a slot
-constexpr uint32_t kFree = 0u, kIssued = 1u, kPrep = 2u;
+constexpr uint32_t kFree = 0u, kIssued = 1u;
 
 struct LatCtl {
   uint32_t done;  // the commit wave has finished the query
@@ -49,7 +49,6 @@ struct LatCtl {
   float coef;
   float radius;
   uint32_t ns;    // serving form: seeds staged in the tail
-  uint32_t expr;  // the commit wave's exploration radius (float bits), for the hop pool
   uint64_t sp[4]; // diagnostic build: speculation-wave cycles ([0] adjacency, [2] exact rows)
 };
 
@@ -64,7 +63,6 @@ struct LatSlot {
   uint32_t deg;    // list length read (getEdgeSize cap), summed over the parts
   uint32_t gen;    // issue generation (the commit wave's)
   uint32_t pn[8];  // neighbours not yet visited when the part was read
-  uint32_t owner;  // pool slots: 0 none, 1 the commit wave (adopted), 2 being recycled
 };
 
 struct LatLayout {
@@ -73,7 +71,7 @@ struct LatLayout {
   __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
   __host__ __device__ LatLayout(const SearchArgs& a, uint32_t cap, uint32_t waves) {
     uint32_t o = up16(sizeof(LatCtl));
-    const uint32_t ns = a.lat_slots + a.lat_pool;
+    const uint32_t ns = a.lat_slots;
     off_slot = o; o = up16(o + sizeof(LatSlot) * ns);
     off_eid = o; o = up16(o + 4u * ns * cap);
     off_ed = o; o = up16(o + 4u * ns * cap);
@@ -329,9 +327,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t NT = 64u * W;
   const uint32_t bm_words = (a.nrows + 31u) / 32u;
-  const uint32_t nslots = a.lat_slots;  // the commit wave's slots
-  const uint32_t npool = a.lat_pool;    // then the hop pool: slots the speculation waves issue themselves
-  const uint32_t nall = nslots + npool;
+  const uint32_t nslots = a.lat_slots;  // speculation slots, issued by the commit wave
   const uint32_t wg = blockIdx.x;
   uint64_t* spill = a.spill + (uint64_t)wg * a.spill_cap;
   const int g = lane & 3, rs = lane >> 2;
@@ -363,11 +359,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
                                                             : a.queries + (uint64_t)qi * a.query_bytes);
       uint4* d = reinterpret_cast<uint4*>(qlds);
       for (uint32_t i = tid; i < (uint32_t)a.dp / 4; i += NT) d[i] = s[i];
-      for (uint32_t i = tid; i < nall; i += NT) {
+      for (uint32_t i = tid; i < nslots; i += NT) {
         slots[i].state = kFree;
         slots[i].claim = 0u;
         slots[i].gen = 0u;
-        slots[i].owner = 0u;
         slots[i].pready = 0u;
       }
       if (tid == 0) {
@@ -410,8 +405,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if ((uint32_t)lane == pos) rk = key;
         nres = nres + 1 < k ? nres + 1 : k;
       };
-      uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0, nadopt = 0;
-      (void)nadopt;
+      uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0;
       (void)nwait;
       // diagnostic build only: shader-clock totals per phase
       uint64_t t_pop = 0, t_wait = 0, t_list = 0, t_feed = 0, t_last = 0;
@@ -419,12 +413,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       float radius = radq;
       uint32_t qerr = 0;  // the batch kernel's error bits, this query's
       float expr = 0.f;
-      // expr, published for the speculation waves' hop choices
-      auto set_expr = [&]() {
-        expr = __fmul_rn(coefq, radius);
-        if (lane == 0)
-          __hip_atomic_store(&ctl->expr, __float_as_uint(expr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      };
+      auto set_expr = [&]() { expr = __fmul_rn(coefq, radius); };
       // unchecked set: head (registers, sorted, hn keys) < B <= tail (LDS,
       // ntail keys) < T <= spill (HBM, nspill keys)
       uint64_t hk = ~0ull;
@@ -630,45 +619,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         hn--;
         return true;
       };
-      // a slot the commit wave is done with: its own slots back to freem, pool
-      // slots back to the pool (unowned, free)
+      // a slot the commit wave is done with goes back to freem
       auto release_slot = [&](uint32_t t) {
-        if (t < nslots) {
-          if (lane == 0) slots[t].state = kFree;
-          freem |= 1ull << t;
-        } else if (lane == 0) {
-          // free before unowned: an unowned issued slot could be taken for a
-          // recycle while a speculation wave still works on it
-          lds_store_rel(&slots[t].state, kFree);
-          lds_store_rel(&slots[t].owner, 0u);
-        }
-      };
-      // a pool slot the speculation waves issued for this key: owned by the
-      // commit wave from here on (CAS on the owner word; the key is re-read
-      // after it, since a recycle may have re-keyed the slot meanwhile)
-      auto adopt = [&](uint64_t key) -> uint32_t {
-        if (npool == 0) return kNoTag;
-        const uint32_t pl = nslots + (uint32_t)lane;
-        const bool c = (uint32_t)lane < npool && lds_load_acq(&slots[pl].state) == kIssued &&
-                       slots[pl].owner == 0u && slots[pl].key == key;
-        uint64_t cm = ballot64(c);
-        while (cm) {
-          const uint32_t t = nslots + (uint32_t)(__ffsll((long long)cm) - 1);
-          cm &= cm - 1;
-          uint32_t ok = 0;
-          if (lane == 0) {
-            uint32_t e = 0u;
-            ok = __hip_atomic_compare_exchange_strong(&slots[t].owner, &e, 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
-          }
-          if (!__builtin_amdgcn_readfirstlane((int)ok)) continue;
-          if (lds_load_acq(&slots[t].state) == kIssued && slots[t].key == key) {
-            nadopt++;
-            return t;
-          }
-          if (lane == 0) lds_store_rel(&slots[t].owner, 0u);
-        }
-        return kNoTag;
+        if (lane == 0) slots[t].state = kFree;
+        freem |= 1ull << t;
       };
       // free the orphaned slots whose speculation has finished
       auto reap = [&]() {
@@ -687,13 +641,14 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       // every wait below is bounded: a slot that never becomes ready (never
       // expected) flags error 16 and ends the query instead of hanging the CU
       bool stuck = false;
-      const uint64_t ownm = nslots >= 64 ? ~0ull : ((1ull << nslots) - 1ull);  // the commit wave's own slots
       auto issue = [&](uint64_t key) -> uint32_t {
-        if (freem == 0ull && (orphan & ownm) == 0ull) {
-          // every own slot is held by a head entry: the node just released was
-          // a pool slot, which goes back to the pool, so nothing comes back to
-          // freem by itself -- the deepest head entry holding an own slot
-          // gives it up (orphaned, freed once its speculation is done)
+        if (freem == 0ull && orphan == 0ull) {
+          // every slot is held by a head entry (tagged entries pushed past the
+          // first F lanes by smaller accepted keys, then F more tagged), and
+          // the node to expand has none: nothing comes back to freem by
+          // itself, so the deepest tagged head entry gives its slot up
+          // (orphaned, freed once its speculation is done; the entry is
+          // issued again when it nears the front)
           const uint64_t om = ballot64(ht < nslots);
           if (om != 0ull) {
             const int l = 63 - __builtin_clzll(om);
@@ -737,12 +692,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           const int l = __ffsll((long long)need) - 1;
           need &= need - 1;
           const uint64_t key = readlane_u64(hk, l);
-          uint32_t s = adopt(key);
-          if (s == kNoTag) {
-            if (freem == 0ull) break;
-            s = issue(key);
-            if (stuck) break;
-          }
+          if (freem == 0ull) break;
+          const uint32_t s = issue(key);
+          if (stuck) break;
           if (lane == l) ht = s;
         }
       };
@@ -830,11 +782,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         if (!pop(key, tag)) break;
         if (key_dist(key) > expr) break;  // Graph.cpp:433-435
         if (tag == kNoTag) {
-          tag = adopt(key);
-          if (tag == kNoTag) {
-            tag = issue(key);
-            nwait++;
-          }
+          tag = issue(key);
+          nwait++;
         }
         if (stuck) break;
         NGT_MARK(t_pop);
@@ -946,71 +895,11 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       }
     } else {
       // =================== speculation waves =================================
-      // issue a pool slot for `key` unless some slot already speculates it:
-      // a free pool slot, else recycle the finished unowned one with the
-      // largest key (when that key is larger than this one)
-      auto hop_issue = [&](uint64_t key) {
-        const bool dup = (uint32_t)lane < nall && slots[lane].key == key && lds_load_acq(&slots[lane].state) == kIssued;
-        if (ballot64(dup)) return;
-        const uint32_t pl = nslots + (uint32_t)lane;
-        const uint32_t pst = (uint32_t)lane < npool ? lds_load_acq(&slots[pl].state) : 0xffu;
-        uint32_t t = ~0u;
-        bool fresh_slot = false;
-        uint64_t fm = ballot64(pst == kFree);
-        while (fm && t == ~0u) {
-          const uint32_t c = nslots + (uint32_t)(__ffsll((long long)fm) - 1);
-          fm &= fm - 1;
-          uint32_t ok = 0;
-          if (lane == 0) {
-            uint32_t e = kFree;
-            ok = __hip_atomic_compare_exchange_strong(&slots[c].state, &e, kPrep, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
-          }
-          if (__builtin_amdgcn_readfirstlane((int)ok)) {
-            t = c;
-            fresh_slot = true;
-          }
-        }
-        if (t == ~0u) {
-          const bool rc = pst == kIssued && slots[pl].owner == 0u && lds_load_acq(&slots[pl].pready) == pfull;
-          const uint64_t rk2 = rc ? slots[pl].key : 0ull;
-          const uint64_t worst = uniform_u64_lat(~wave_min_u64(~rk2));
-          if (worst <= key) return;  // every finished slot is a better bet
-          const uint32_t c = nslots + (uint32_t)(__ffsll((long long)ballot64(rc && rk2 == worst)) - 1);
-          uint32_t ok = 0;
-          if (lane == 0) {
-            uint32_t e = 0u;
-            ok = __hip_atomic_compare_exchange_strong(&slots[c].owner, &e, 2u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
-          }
-          if (!__builtin_amdgcn_readfirstlane((int)ok)) return;
-          // still finished and issued under the lock (only a free slot changes state otherwise)
-          if (lds_load_acq(&slots[c].state) != kIssued || lds_load_acq(&slots[c].pready) != pfull) {
-            if (lane == 0) lds_store_rel(&slots[c].owner, 0u);
-            return;
-          }
-          t = c;
-        }
-        const uint32_t gen = (slots[t].gen + 1u) & 0xffffffu;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          slots[t].key = key;
-          slots[t].pready = 0u;
-          slots[t].deg = 0u;
-          slots[t].gen = gen;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          lds_store_rel(&slots[t].claim, gen << 8);
-          lds_store_rel(&slots[t].owner, 0u);
-          if (fresh_slot) lds_store_rel(&slots[t].state, kIssued);
-        }
-      };
       for (;;) {
         if (lds_load_acq(&ctl->done)) break;
         // the issued slot with the smallest key
-        const uint32_t st = (uint32_t)lane < nall ? lds_load_acq(&slots[lane].state) : kFree;
-        const uint32_t cw = (uint32_t)lane < nall ? lds_load_acq(&slots[lane].claim) : 0u;
+        const uint32_t st = (uint32_t)lane < nslots ? lds_load_acq(&slots[lane].state) : kFree;
+        const uint32_t cw = (uint32_t)lane < nslots ? lds_load_acq(&slots[lane].claim) : 0u;
         const uint64_t cand = st == kIssued && (cw & 0xffu) < parts ? slots[lane].key : ~0ull;
         const uint64_t m = uniform_u64_lat(wave_min_u64(cand));
         if (m == ~0ull) {
@@ -1057,9 +946,6 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         // the comparator's exact distances of those neighbours
         // (PrimitiveComparator::compareL2 through l2_fold_rows): a quad per
         // row, EG groups of 16 rows in flight
-        // the smallest key among them within the exploration radius: the
-        // neighbour the commit wave most likely accepts and pops soon (hop)
-        uint64_t hop = ~0ull;
         {
           const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
           for (uint32_t r0 = 0; r0 < np; r0 += 16u * EG) {
@@ -1075,21 +961,12 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
 #pragma unroll
               for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
             }
-            const float ex = npool ? __uint_as_float(__hip_atomic_load(&ctl->expr, __ATOMIC_RELAXED,
-                                                                       __HIP_MEMORY_SCOPE_WORKGROUP))
-                                   : 0.f;
 #pragma unroll
             for (int j = 0; j < EG; j++) {
               if (r0 + 16u * j >= np) continue;
               const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
               const float d = l2_fold_rows<NCH>(qq, v[j]);
-              if (g == 0 && rr < np) {
-                sd[rr] = d;
-                if (d <= ex) {
-                  const uint64_t kk = make_key(d, rid[j]);
-                  hop = kk < hop ? kk : hop;
-                }
-              }
+              if (g == 0 && rr < np) sd[rr] = d;
             }
           }
         }
@@ -1106,10 +983,6 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         // bit is set, the commit wave may free and reissue it
         if (lane == 0)
           __hip_atomic_fetch_or(&slots[sl].pready, 1u << part, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (npool) {
-          hop = uniform_u64_lat(wave_min_u64(hop));
-          if (hop != ~0ull) hop_issue(hop);
-        }
       }
     }
     __syncthreads();

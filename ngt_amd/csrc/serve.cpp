@@ -62,7 +62,7 @@ struct ServeConfig {
   const void* pivot;
   const void* leaf_ids;
   uint64_t nrows, adj_stride, es, rows_version, adj_version, tree_version;
-  int32_t use_tree, all_leaf, seed_size, lat_slots, lat_tail, lat_pool;
+  int32_t use_tree, all_leaf, seed_size, lat_slots, lat_tail;
   bool operator==(const ServeConfig& o) const { return memcmp(this, &o, sizeof o) == 0; }
 };
 
@@ -97,6 +97,7 @@ struct Server {
   uint32_t next = 0;
   std::vector<uint8_t> busy;
   int inflight = 0;  // under mu
+  bool hold = false;  // under mu: the index is changing, callers take the launch path
   std::atomic<uint64_t> served{0}, launches{0};
   bool log = false;  // NGT_AMD_SERVE_LOG=1: a stderr line per grid
   std::chrono::steady_clock::time_point t_launch;
@@ -133,7 +134,8 @@ int server_init(ngt_amd_index* ix, Server* sv) {
   sv->busy.assign(sv->nring, 0);
   HIP_OK(sv->dctl.alloc(1));
   HIP_OK(sv->err.alloc(1));
-  HIP_OK(hipMemset(sv->err.p, 0, sizeof(int)));
+  HIP_OK(hipMemsetAsync(sv->err.p, 0, sizeof(int), sv->s));
+  HIP_OK(hipStreamSynchronize(sv->s));
   const char* v = getenv("NGT_AMD_SERVE_WORKERS");
   const int w = v ? atoi(v) : 128;
   sv->workers = (uint32_t)std::max(1, std::min(w, ix->cu_count - 1));
@@ -248,20 +250,10 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   const size_t lds_max = std::max<size_t>(64 * 1024, std::min<size_t>(ix->lds_per_block, ix->lds_per_cu));
   a.lat_slots = cap <= 64 ? 32u : 16u;
   a.lat_tail = 4096u;
-  {
-    // the hop pool (search_lat.hip): NGT_AMD_LAT_POOL slots, 0 = off (the
-    // default; see ngt_amd_api.cpp)
-    const int pool = [] {
-      const char* v = getenv("NGT_AMD_LAT_POOL");
-      return v ? std::max(0, std::min(32, atoi(v))) : 0;
-    }();
-    a.lat_pool = (uint32_t)std::max(0, std::min(pool, 64 - (int)a.lat_slots));
-  }
   while (search_lat_lds_bytes(a) > lds_max && a.lat_tail > 512u) a.lat_tail -= 256u;
   while (search_lat_lds_bytes(a) > lds_max && a.lat_slots > 8u) a.lat_slots -= 2u;
   if (const char* v = getenv("NGT_AMD_LAT_TAIL")) a.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
   if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) a.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
-  a.lat_pool = std::min<uint32_t>(a.lat_pool, 64u - a.lat_slots);
   if (search_lat_lds_bytes(a) > lds_max) return 1;
   cfg = ServeConfig{};
   cfg.rows = ix->rows.p;
@@ -279,11 +271,33 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   cfg.seed_size = tree ? std::max(ix->seed_size, 0) : 0;
   cfg.lat_slots = (int32_t)a.lat_slots;
   cfg.lat_tail = (int32_t)a.lat_tail;
-  cfg.lat_pool = (int32_t)a.lat_pool;
   return 0;
 }
 
 }  // namespace
+
+// The index is about to change (rows, graph, padded adjacency, tree): new
+// served calls take the launch path, the calls in flight finish, and the grid
+// leaves -- it holds the old buffers' pointers, and so does the relaunch
+// state sv->a.  The next served call relaunches with the index's new state.
+// The callers in flight never take ix->mu, so a caller holding it may wait here.
+void serve_quiesce(ngt_amd_index* ix) {
+  Server* sv = ix->serve;
+  if (!sv) return;
+  for (bool first = true;; first = false) {
+    {
+      std::lock_guard<std::mutex> lk(sv->mu);
+      if (first) sv->hold = true;
+      if (sv->inflight == 0) {
+        (void)server_reap(sv, true);
+        sv->cfg = ServeConfig{};
+        sv->hold = false;
+        return;
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
 
 void serve_destroy(ngt_amd_index* ix) {
   Server* sv = ix->serve;
@@ -327,6 +341,7 @@ extern "C" int ngt_amd_search_served(ngt_amd_index* ix, const ngt_amd_search_par
   // join the grid's configuration, or switch it when nothing is in flight
   {
     std::lock_guard<std::mutex> lk(sv->mu);
+    if (sv->hold) return 1;
     if (!(sv->cfg == cfg)) {
       if (sv->inflight > 0) return 1;
       if (server_reap(sv, true)) return -1;
@@ -410,7 +425,8 @@ extern "C" int ngt_amd_search_served(ngt_amd_index* ix, const ngt_amd_search_par
       if (now - t0 > std::chrono::seconds(60)) return fail("ngt_amd_search_served: no answer from the serving grid");
     }
   }
-  if (r->err) return fail("ngt_amd_search_served: device error flag %u (unchecked-set spill capacity exceeded)", r->err);
+  if (r->err)
+    return fail("ngt_amd_search_served: device error flag %u (%s)", r->err, device_error_text((int)r->err).c_str());
   const uint32_t nr = std::min(r->n, prm->k);
   memcpy(ids, r->ids, 4ull * nr);
   memcpy(dists, r->dists, 4ull * nr);

@@ -55,7 +55,8 @@ extern "C" int ngt_amd_shard_comm_create(ngt_amd_shard_comm** out, int device, i
   c->device = device;
   c->rank = rank;
   c->world = world;
-  if (c->err.alloc(1) != hipSuccess || hipMemset(c->err.p, 0, sizeof(int)) != hipSuccess) {
+  if (c->err.alloc(1) != hipSuccess || hipMemsetAsync(c->err.p, 0, sizeof(int), nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
     delete c;
     return fail("ngt_amd_shard_comm_create: allocation failed");
   }
@@ -142,8 +143,8 @@ extern "C" int ngt_amd_shard_comm_synchronize(ngt_amd_shard_comm* c, void* strea
   if (flag) {
     HIP_OK(hipMemsetAsync(c->err.p, 0, sizeof(int), s));
     HIP_OK(hipStreamSynchronize(s));
-    return fail("sharded search: a shard's search flagged device error %d (unchecked-set spill capacity "
-                "exceeded): its result list was truncated", flag);
+    return fail("sharded search: a shard's search flagged device error %d (%s)", flag,
+                device_error_text(flag).c_str());
   }
   return 0;
 }

@@ -160,35 +160,54 @@ class ShardedIndex(object):
 
     def _out(self, nq, k):
         t = self.torch
-        return (t.zeros((nq, k), dtype=t.int32, device=self.device), t.zeros((nq, k), dtype=t.float32, device=self.device),
-                t.zeros((nq,), dtype=t.int32, device=self.device))
+        S = len(self.indexes)
+        lead = (S,) if S > 1 else ()
+        return (t.zeros(lead + (nq, k), dtype=t.int32, device=self.device),
+                t.zeros(lead + (nq, k), dtype=t.float32, device=self.device),
+                t.zeros(lead + (nq,), dtype=t.int32, device=self.device))
+
+    def _each(self, seeds, seed_off):
+        """(index, slice selector) for every local shard; given seeds name one
+        shard's local ids, so they are taken only with one local shard."""
+        if len(self.indexes) > 1 and seeds is not None:
+            raise ValueError("ShardedIndex: given seeds are local ids of one shard; with %d local shards use tree "
+                             "or random seeds, or search each shard and call merge_local" % len(self.indexes))
+        if len(self.indexes) == 1:
+            return [(self.indexes[0], None)]
+        return [(ix, s) for s, ix in enumerate(self.indexes)]
 
     def search_device(self, d_queries, query_bytes, nq, k, epsilon, seeds=None, seed_off=None, stream=None,
                       visited_hash_log2=0, edge_size=-1, seed_mode=None):
-        """Local graph search of nq device queries on this shard, then the
-        exchange and merge; returns global (ids, dists, n) tensors."""
+        """Local graph search of nq device queries on every local shard (one
+        after another on `stream`), then the exchange and merge; returns
+        global (ids, dists, n) tensors."""
         from .device import SEED_GIVEN, SEED_TREE
         with self._on(stream):  # the outputs' zero-fill is ordered before the search on `stream`
             ids, ds, n = self._out(nq, k)
         mode = seed_mode if seed_mode is not None else (SEED_GIVEN if seeds is not None else SEED_TREE)
-        self.index.search_device(d_queries, query_bytes, nq, ids.data_ptr(), ds.data_ptr(), n.data_ptr(), None,
-                                 k=k, epsilon=epsilon, edge_size=edge_size, seed_mode=mode, d_seeds=seeds,
-                                 d_seed_off=seed_off, stream=stream, visited_hash_log2=visited_hash_log2)
+        for ix, s in self._each(seeds, seed_off):
+            oi, od, on = (ids, ds, n) if s is None else (ids[s], ds[s], n[s])
+            ix.search_device(d_queries, query_bytes, nq, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None,
+                             k=k, epsilon=epsilon, edge_size=edge_size, seed_mode=mode, d_seeds=seeds,
+                             d_seed_off=seed_off, stream=stream, visited_hash_log2=visited_hash_log2)
         return self.merge_local(ids, ds, n, k, stream)
 
     def qg_search_device(self, d_queries, query_bytes, nq, k, epsilon, result_expansion=3.0, seeds=None,
                          seed_off=None, stream=None, visited_hash_log2=-1, seed_mode=None):
         """C5's form: the NGTQG search (QuantizedGraph.h:354-372) of nq device
-        queries on this shard's quantized graph (exact rerank of k * expansion
-        included), then the same exchange and merge of the reranked top-k."""
+        queries on every local shard's quantized graph (exact rerank of
+        k * expansion included), then the same exchange and merge of the
+        reranked top-k."""
         from .device import SEED_GIVEN, SEED_TREE
         with self._on(stream):
             ids, ds, n = self._out(nq, k)
         mode = seed_mode if seed_mode is not None else (SEED_GIVEN if seeds is not None else SEED_TREE)
-        self.index.qg_search_device(d_queries, query_bytes, nq, ids.data_ptr(), ds.data_ptr(), n.data_ptr(), None,
-                                    k=k, epsilon=epsilon, result_expansion=result_expansion, seed_mode=mode,
-                                    d_seeds=seeds, d_seed_off=seed_off, stream=stream,
-                                    visited_hash_log2=visited_hash_log2)
+        for ix, s in self._each(seeds, seed_off):
+            oi, od, on = (ids, ds, n) if s is None else (ids[s], ds[s], n[s])
+            ix.qg_search_device(d_queries, query_bytes, nq, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None,
+                                k=k, epsilon=epsilon, result_expansion=result_expansion, seed_mode=mode,
+                                d_seeds=seeds, d_seed_off=seed_off, stream=stream,
+                                visited_hash_log2=visited_hash_log2)
         return self.merge_local(ids, ds, n, k, stream)
 
 

@@ -81,23 +81,30 @@ def test_sample_compiles_and_reads_accuracy_table(sample):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pool", [None])
-def test_cxx_search_matches_reference(sample, monkeypatch, pool):
+def test_cxx_search_matches_reference(sample):
     """Single-query searches through the C++ facade (the serving grid of the
-    latency kernel).  With an 8-slot hop pool (NGT_AMD_LAT_POOL=8, opt-in)
-    this search stopped with error 16 before the own-slot steal in
-    search_lat.hip; add "8" to the pool list once that is confirmed on a GPU
-    (scripts/gpu_r3w.sh runs it)."""
-    if pool is not None:
-        monkeypatch.setenv("NGT_AMD_LAT_POOL", pool)
+    latency kernel): ids and distance counts equal the reference's goldens,
+    and the distance bits equal the pinned oracle's restatement of
+    NeighborhoodGraph::search over the same index (the goldens hold the
+    reference CLI's printed distances, 6 significant digits)."""
     exe, qf, d = sample
     ids, ds, nd, first = parse(run(exe, "search", os.path.join(GOLD, "c1_anng"), qf, 10, 0.1), 100, 10)
     g = np.load(os.path.join(GOLD, "search_c1_anng_tw_0.1.npz"))
-    rows, _ = F.read_obj(os.path.join(GOLD, "c1_anng", "obj"), 128, np.float32)
+    name = os.path.join(GOLD, "c1_anng")
+    prop = F.read_prf(os.path.join(name, "prf"))
+    rows, _ = F.read_obj(os.path.join(name, "obj"), 128, np.float32)
+    offs, gids, _ = F.read_grp(os.path.join(name, "grp"))
+    tree = F.read_tre(os.path.join(name, "tre"), 128, np.float32)
+    es = int(prop["EdgeSizeForSearch"])
+    qs = np.load(os.path.join(GOLD, "queries.npy")).astype(np.float32)
     for i in range(100):
         ref = g["ids"][i][g["ids"][i] >= 0]
         assert list(ids[i, :len(ref)]) == list(ref), i
         assert ["%g" % x for x in ds[i, :len(ref)]] == ["%g" % x for x in g["dists"][i][:len(ref)]], i
+        seeds, _, _ = O.tree_seeds("l2", tree, qs[i], 10, int(prop["SeedSize"]))
+        oid, od, _ = O.search("l2", rows, offs, gids, qs[i], seeds, 10, np.float32(0.1), edge_size=es)
+        assert list(oid) == list(ref), i
+        assert np.array_equal(ds[i, :len(ref)].view(np.uint32), od.view(np.uint32)), i
         # sc.distanceComputationCount of the reference's read-write search
         assert nd[i] == int(g["ndist"][i]), i
         assert first[i] == int(rows[ref[0], 0].view(np.uint32))  # getObjectSpace().getObject

@@ -130,14 +130,15 @@ def test_lookahead_equals_single_expansion_kernel(monkeypatch, name):
 
 @pytest.mark.parametrize("knobs", [{"NGT_AMD_LAT_TAIL": "128"}, {"NGT_AMD_LAT_SLOTS": "2"},
                                    {"NGT_AMD_LAT_SLOTS": "3", "NGT_AMD_LAT_TAIL": "256"},
-                                   {"NGT_AMD_LAT_POOL": "0"}, {"NGT_AMD_LAT_POOL": "2", "NGT_AMD_LAT_SLOTS": "4"}])
+                                   {"NGT_AMD_LAT_SLOTS": "4"}, {"NGT_AMD_LAT_SLOTS": "6", "NGT_AMD_LAT_TAIL": "512"}])
 @pytest.mark.parametrize("deg", [24, 150])
 def test_latency_kernel_spill_and_slots(monkeypatch, knobs, deg):
     """The speculating latency kernel (search_lat.hip) with a tail small
     enough to push keys to the HBM spill and refill from it, with so few
-    speculation slots that head entries lose theirs (orphaned slots reaped),
-    without the hop pool and with a two-slot pool (recycled constantly): ids,
-    distance bits and the reference's distance/expansion counts."""
+    speculation slots that head entries lose theirs (orphaned slots reaped,
+    and the deepest tagged head entry gives its slot up when every slot is
+    held and the node to expand has none): ids, distance bits and the
+    reference's distance/expansion counts."""
     for kv in knobs.items():
         monkeypatch.setenv(*kv)
     monkeypatch.setenv("NGT_AMD_LA", "2")

@@ -60,7 +60,25 @@ def numpy_merge(torch, g_packed, offsets, k, stream=None):
     return out_i, out_d, out_n
 
 
-def _worker(rank, world, port, q, per_rank=1):
+class _Shard(object):
+    """Stand-in for a DeviceIndex on CPU tensors: search_device writes the
+    shard's precomputed local results through the output pointers, as the
+    library writes device memory."""
+
+    def __init__(self, ids, ds, n):
+        self.ids, self.ds, self.n = ids, ds, n
+        self.calls = 0
+
+    def search_device(self, d_queries, query_bytes, nq, d_ids, d_dists, d_n, d_counters, **kw):
+        import ctypes
+        assert nq == self.n.shape[0]
+        ctypes.memmove(d_ids, self.ids.ctypes.data, self.ids.nbytes)
+        ctypes.memmove(d_dists, self.ds.ctypes.data, self.ds.nbytes)
+        ctypes.memmove(d_n, self.n.ctypes.data, self.n.nbytes)
+        self.calls += 1
+
+
+def _worker(rank, world, port, q, per_rank=1, via_search=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -86,7 +104,14 @@ def _worker(rank, world, port, q, per_rank=1):
             all_ids.append(ids)
             all_ds.append(ds)
             all_n.append(n)
-        if per_rank == 1:
+        if via_search:
+            # ShardedIndex.search_device searches EVERY local shard
+            shards = [_Shard(all_ids[s], all_ds[s], all_n[s]) for s in range(per_rank)]
+            sx = ShardedIndex(torch, dist, shards if per_rank > 1 else shards[0], offs if per_rank > 1 else offs[0],
+                              torch.device("cpu"), pack=numpy_pack, merge=numpy_merge)
+            gi, gd, gn = sx.search_device(None, 0, NQ, K, 0.1)
+            assert all(sh.calls == 1 for sh in shards)
+        elif per_rank == 1:
             sx = ShardedIndex(torch, dist, None, offs[0], torch.device("cpu"), pack=numpy_pack, merge=numpy_merge)
             gi, gd, gn = sx.merge_local(torch.from_numpy(all_ids[0]), torch.from_numpy(all_ds[0]),
                                         torch.from_numpy(all_n[0]), K)
@@ -118,15 +143,17 @@ def test_shard_bounds_partition():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("per_rank", [1, 3])
-def test_sharded_search_equals_union_gloo(per_rank):
+@pytest.mark.parametrize("per_rank,via_search", [(1, False), (3, False), (1, True), (3, True)])
+def test_sharded_search_equals_union_gloo(per_rank, via_search):
     """world 2; per_rank 3: every rank holds three shards (C4/C5's index
-    served as several shards per GPU), six lists merged per query."""
+    served as several shards per GPU), six lists merged per query.
+    via_search: through ShardedIndex.search_device, which must search every
+    local shard (not only the first) before the one all-gather."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, per_rank)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, per_rank, via_search)) for r in range(2)]
     for p in procs:
         p.start()
     import queue
