@@ -252,6 +252,9 @@ def main():
     ap.add_argument("--pmc-launches", type=int, default=0,
                     help="after the epsilon is set: run this many launches of the timed configuration and exit")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
+    ap.add_argument("--anng-line", choices=["auto", "on", "off"], default="auto",
+                    help="attach the NGT-built index's line (a child run of --graph anng) as the 'anng' key; "
+                         "auto = on for the default single-GPU C2 run")
     ap.add_argument("--visited", type=int, default=-2,
                     help="visited set: -2 HBM epochs of accepted ids, -1 HBM epochs of every evaluated id "
                          "(C2 visits ~1e5 ids/query), 0 LDS hash")
@@ -546,6 +549,17 @@ def main():
         alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + NQ * (dp * 4 + K * 8)
         kname = "ngt_graph_search_kernel"
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    split = None
+    if filtered and not qgm:
+        # where the algorithmic bytes come from: the 1-byte filter copy (N x Dp
+        # bytes, 128 MB at C2 -- a table the 256 MiB Infinity Cache holds) and
+        # the f32 rows, adjacency, queries and results (tables beyond it)
+        fbytes = (c[:, 0] - c[:, 7]).sum() * dp
+        mall_table = (N + 1) * dp
+        split = {"filter_copy_bytes": fbytes, "filter_copy_table_bytes": mall_table,
+                 "filter_copy_fits_infinity_cache": mall_table <= 256 * 2 ** 20,
+                 "other_bytes": alg_bytes - fbytes,
+                 "other_gbs": (alg_bytes - fbytes) / (kernel_ms * 1e-3) / 1e9}
     traffic, tentry = measured_traffic(args.mode, args.config, graph, chosen, args.visited, filtered)
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "exact":
         tot = c[:, [5, 6, 1, 7, 3]].mean(0)
@@ -675,7 +689,8 @@ def main():
                          # the same bytes over the whole step with launches overlapping on the streams
                          # (a single launch's last round of queries leaves the GPU part-empty)
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
-                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS},
+                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
+                         "bytes_split": split},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "sweep": sweep,
@@ -698,6 +713,12 @@ def main():
                 "source": tentry.get("source", ""), "SQ_INSTS_VALU": cn["SQ_INSTS_VALU"],
                 "valu_wave_cycle_frac": cn["SQ_ACTIVE_INST_VALU"] / cn["SQ_WAVE_CYCLES"],
                 "traffic_over_algorithmic": traffic / alg_bytes}
+            if "TCC_HIT_sum" in cn:
+                line["roofline"]["counters"].update({
+                    "l2_hit_rate": tentry.get("l2_hit_rate"),
+                    "dram_destined_read_frac": tentry.get("dram_destined_read_frac"),
+                    "note": "FETCH_SIZE and TCC_EA0_RDREQ_DRAM count the L2's memory-side reads, Infinity-Cache "
+                            "hits included; no TCC counter on gfx950 separates them"})
             if "SQ_WAIT_ANY" in cn:
                 # the wave-cycle partition (MI355X_MICROARCH.md rocprofv3 PMC slots):
                 # parked on s_waitcnt/barrier, issue-stalled, issuing
@@ -707,6 +728,14 @@ def main():
                     "active_inst_any_frac": cn["SQ_ACTIVE_INST_ANY"] / w,
                     "SQ_INSTS_LDS": cn.get("SQ_INSTS_LDS"),
                     "trace_avg_kernel_ms": tentry.get("trace_avg_kernel_ms")})
+                # what bounds the kernel, from the wave-cycle partition: more
+                # than half the wave-cycles parked on s_waitcnt = the
+                # dependent-gather latency, not the bytes' rate
+                if cn["SQ_WAIT_ANY"] / w >= 0.5:
+                    line["roofline"]["bound"] = "latency"
+                    line["roofline"]["bound_note"] = (
+                        "wait_any_frac >= 0.5: dependent gathers, not HBM bandwidth; achieved/peak still against "
+                        "the 8 TB/s HBM figure")
         if qgm:
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
@@ -718,9 +747,44 @@ def main():
                 line["config"]["exact_neighbour_distances_per_query"] = float(c[:, 6].mean())
             if evals_per_query is not None:
                 line["config"]["evaluations_per_query"] = evals_per_query
+        want_anng = args.anng_line == "on" or (args.anng_line == "auto" and args.mode == "exact" and not c3
+                                               and args.graph == "knn" and world == 1)
+        if want_anng:
+            line["anng"] = anng_child_line(args)
         print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def anng_child_line(args):
+    """The index a `ngt create` user has, measured beside the headline: the
+    1M ANNG (E 10) built on the device through the C API (files identical to
+    the reference's build), searched at the prf's EdgeSizeForSearch 40
+    (Command.cpp:39, Graph.h:675-692) from DVP-tree seeds.  A child process
+    of this bench (`--graph anng`), so its line carries its own roofline,
+    cpu_baseline, parity sample and reference checks; None if it fails."""
+    import subprocess
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--graph", "anng", "--anng-line", "off",
+           "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1", "--cpu-seconds", str(min(args.cpu_seconds, 8.0)),
+           "--latency-queries", "20"]
+    if args.no_cpu:
+        cmd.append("--no-cpu")
+    t0 = time.time()
+    log("ANNG line: %s" % " ".join(cmd[2:]))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=env, timeout=900)
+    out = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not out:
+        log("ANNG line failed (rc %d)" % r.returncode)
+        return {"error": "child run failed", "rc": r.returncode}
+    d = json.loads(out[-1])
+    d.pop("sweep", None)
+    d["child_wall_s"] = time.time() - t0
+    log("ANNG line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
+        d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
+    return d
 
 
 def measured_traffic(mode, config, graph, eps, visited, filtered=False):
@@ -1218,13 +1282,49 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": per_launch,
                          "what": "one shard's search launch alone (mean over the %d local shards)" % S,
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
-                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS},
+                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
+                         "bytes_split": split},
             "cpu_baseline": cpu, "parity_sample": parity, "sweep": sweep}
         if qgm:
             line["config"]["result_expansion"] = args.expansion
+        want_anng = args.anng_line == "on" or (args.anng_line == "auto" and args.mode == "exact" and not c3
+                                               and args.graph == "knn" and world == 1)
+        if want_anng:
+            line["anng"] = anng_child_line(args)
         print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def anng_child_line(args):
+    """The index a `ngt create` user has, measured beside the headline: the
+    1M ANNG (E 10) built on the device through the C API (files identical to
+    the reference's build), searched at the prf's EdgeSizeForSearch 40
+    (Command.cpp:39, Graph.h:675-692) from DVP-tree seeds.  A child process
+    of this bench (`--graph anng`), so its line carries its own roofline,
+    cpu_baseline, parity sample and reference checks; None if it fails."""
+    import subprocess
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--graph", "anng", "--anng-line", "off",
+           "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1", "--cpu-seconds", str(min(args.cpu_seconds, 8.0)),
+           "--latency-queries", "20"]
+    if args.no_cpu:
+        cmd.append("--no-cpu")
+    t0 = time.time()
+    log("ANNG line: %s" % " ".join(cmd[2:]))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=env, timeout=900)
+    out = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not out:
+        log("ANNG line failed (rc %d)" % r.returncode)
+        return {"error": "child run failed", "rc": r.returncode}
+    d = json.loads(out[-1])
+    d.pop("sweep", None)
+    d["child_wall_s"] = time.time() - t0
+    log("ANNG line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
+        d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
+    return d
 
 
 def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):

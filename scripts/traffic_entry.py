@@ -2,7 +2,9 @@
 """Per-launch counter figures of one search kernel from the pmc_r3.sh
 summaries (<dir>/<name>_{fetch,write,sq}_pmc.json + <name>_kernel_stats.csv),
 appended to profiles/traffic.json (an entry with the same workload key is
-replaced).  Units (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE and
+replaced); with a <name>_tcc_pmc.json (scripts/pmc_r4.sh) also the L2 hit rate
+and the DRAM-destined share of the L2's memory-side reads.  Units
+(MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE and
 WRITE_SIZE are KiB; FETCH_SIZE is doubled (gfx950 tallies 128-B requests at
 64 B); SQ_* cycle counters are quad-cycles.
   traffic_entry.py <dir> <name> <kernel-substring> key=value ...  (graph=..., epsilon=..., mode=..., config=...)"""
@@ -37,6 +39,14 @@ assert wr["dispatches"] == n and sq["dispatches"] == n
 fetch = fe["FETCH_SIZE"] / n * 1024 * 2
 write = wr["WRITE_SIZE"] / n * 1024
 per = {c: v / n for c, v in sq.items() if c.startswith("SQ_")}
+tcc = None
+if os.path.exists(os.path.join(d, "%s_tcc_pmc.json" % name)):
+    # L2 hit rate and the share of L2 memory-side read requests destined for
+    # DRAM (the Infinity Cache sits behind that interface: its hits count)
+    _, tc = pick("tcc")
+    assert tc["dispatches"] == n
+    tcc = {c: v / n for c, v in tc.items() if c.startswith("TCC_")}
+    per.update(tcc)
 avg_ns = None
 with open(os.path.join(d, name + "_kernel_stats.csv")) as f:
     for row in csv.DictReader(f):
@@ -47,9 +57,13 @@ e.update({"kernel": kname.replace("void ngt_amd::", ""), "fetch_bytes": fetch, "
           "traffic_bytes": fetch + write, "counters_per_launch": per,
           "trace_avg_kernel_ms": avg_ns / 1e6 if avg_ns else None,
           "source": "%s/%s_{fetch,write,sq}_pmc.json, %s_kernel_stats.csv (scripts/pmc_r3.sh: rocprofv3 "
-                    "--kernel-trace --stats, then separate --pmc passes FETCH_SIZE | WRITE_SIZE | %s; %d dispatches "
+                    "--kernel-trace --stats, then separate --pmc passes FETCH_SIZE | WRITE_SIZE | %s%s; %d dispatches "
                     "of the timed configuration each; FETCH_SIZE x1024 x2, WRITE_SIZE x1024)" % (
-                        d, name, name, " ".join(sorted(per)), n)})
+                        d, name, name, " ".join(sorted(c for c in per if c.startswith("SQ_"))),
+                        (" | " + " ".join(sorted(tcc))) if tcc else "", n)})
+if tcc:
+    e["l2_hit_rate"] = tcc["TCC_HIT_sum"] / max(1.0, tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"])
+    e["dram_destined_read_frac"] = tcc["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, tcc["TCC_EA0_RDREQ_sum"])
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
 t = json.load(open(path))
 DEF = {"mode": "exact", "config": "c2", "graph": None, "epsilon": None, "visited": -1, "filtered": False}
