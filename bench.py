@@ -291,7 +291,7 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    from ngt_amd.device import COUNTERS, SEED_GIVEN, DeviceIndex
+    from ngt_amd.device import COUNTERS, SEED_GIVEN, SEED_TREE, DeviceIndex
     if args.mode == "capi":
         return capi_bench(args, torch, dev, result_out)
     if args.mode == "shard":
@@ -462,6 +462,42 @@ def main():
         chosen = float(t.item())
         rec = measure(chosen, NQ)
 
+    order_exp = os.environ.get("NGT_BENCH_ORDER", "")
+    if order_exp and not shard and not qgm:
+        # EXPERIMENT (never the product line): the single launch's tail against
+        # the order queries are pulled in.  "oracle": longest first by the
+        # expansions of the last run; "centroid": by the query's distance to
+        # the data's mean (a cheap predictor).  Prints per-order kernel times.
+        run(chosen)
+        torch.cuda.synchronize()
+        ne0 = cnt[:, 2].cpu().numpy().astype(np.float64)
+        cen = rows[1:, :D].mean(0)
+        dc = (qdev[:, :D] - cen).norm(dim=1).cpu().numpy()
+        rr = np.corrcoef(dc, ne0)[0, 1]
+        log("order experiment: corr(expansions, |q - mean|) = %.3f" % rr)
+        dump = os.environ.get("NGT_BENCH_DUMP")
+        if dump:
+            np.savez(dump, expansions=ne0, counters=cnt.cpu().numpy(), epsilon=chosen, centroid_dist=dc)
+        tree_mode = args.seeds == "tree"
+        for name, perm in (("given", np.arange(NQ)), ("oracle", np.argsort(-ne0, kind="stable")),
+                           ("centroid_asc", np.argsort(dc, kind="stable")),
+                           ("centroid_desc", np.argsort(-dc, kind="stable"))):
+            pt = torch.from_numpy(perm).to(dev)
+            q2 = qdev[pt].contiguous()
+            s2 = None if tree_mode else d_seeds.view(NQ, -1)[pt].contiguous().view(-1)
+            ts = []
+            for _ in range(3):
+                oi, od, on, oc = bufs[0]
+                ix.search_device(q2.data_ptr(), dp * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                                 oc.data_ptr(), k=K, epsilon=chosen, edge_size=args.edge_size,
+                                 seed_mode=SEED_TREE if tree_mode else SEED_GIVEN,
+                                 d_seeds=None if tree_mode else s2.data_ptr(),
+                                 d_seed_off=None if tree_mode else d_soff.data_ptr(), stream=streams[0],
+                                 visited_hash_log2=args.visited)
+                torch.cuda.synchronize()
+                ts.append(ix.last_search_kernel_ms())
+            log("order %s: kernel %.2f ms (min of 3: %.2f)" % (name, float(np.mean(ts)), float(np.min(ts))))
+        return
     if args.pmc_launches:
         # counter passes (scripts/pmc_r3.sh): exactly this many more launches of
         # the timed configuration, nothing else of the bench
@@ -548,6 +584,8 @@ def main():
         # B(q) = U(q)*Dp*4 + E(q)*4 + Dp*4 + k*8   
         alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + NQ * (dp * 4 + K * 8)
         kname = "ngt_graph_search_kernel"
+    if not qgm and la_form >= 0:
+        kname = "ngt_graph_search_la_kernel"  # the lookahead kernel (search_la.hip) ran the timed launches
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     split = None
     if filtered and not qgm:
