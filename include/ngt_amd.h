@@ -208,6 +208,13 @@ int ngt_amd_last_search_filtered(const ngt_amd_index *index);
 /* Workgroups (resident one-wave query slots) of the last search launch: per-CU
  * occupancy x CUs for a full batch, bounded by the visited-scratch HBM budget. */
 uint32_t ngt_amd_last_search_slots(const ngt_amd_index *index);
+/* Launch schedule of the last search call: 0 = one launch in query order;
+ * B > 0 = "probe and resume" -- a probe launch paused every query after B
+ * expansions (saving its state and the unchecked keys within its exploration
+ * radius as the predicted rest of its search) and a resume launch ran the
+ * paused ones longest-predicted first, so long searches do not start last
+ * (NGT_AMD_SCHED=0 turns it off; results are the same either way). */
+uint32_t ngt_amd_last_search_budget(const ngt_amd_index *index);
 
 /* ---- ANNG construction --------------------------------------------------- *
  *   ngt_amd_build_begin / _insert <- GraphAndTreeIndex::createIndex(threadPoolSize)

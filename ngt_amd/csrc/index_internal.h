@@ -109,9 +109,25 @@ struct SearchCtx {
   DevBuf<uint32_t> ivf_cid, ivf_cn;  // NGTQ: global-codebook search results [nq][cbs], [nq]
   DevBuf<float> ivf_cd;
   DevBuf<int> err;               // device error flag of the launches on this stream
+  // launch schedule ("probe and resume", ngt_amd_api.cpp run_search): the
+  // paused queries' states, flags, predictions and the resume order; the
+  // mean expansions per query of earlier launches of the same configuration
+  // (a pinned copy of the device sums, read once the launch has finished)
+  DevBuf<uint8_t> qstate;
+  DevBuf<uint32_t> qflag, order;
+  DevBuf<float> prio;
+  DevBuf<unsigned long long> stat;
+  unsigned long long* h_stat = nullptr;
+  hipEvent_t ev_stat = nullptr;
+  bool stat_pending = false;
+  uint64_t stat_key = 0;
+  std::vector<std::pair<uint64_t, double>> sched_mean;
+  uint32_t launch_budget = 0;
   ~SearchCtx() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (ev_stat) (void)hipEventDestroy(ev_stat);
+    if (h_stat) (void)hipHostFree(h_stat);
   }
 };
 

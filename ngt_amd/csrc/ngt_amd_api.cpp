@@ -489,6 +489,33 @@ static int lookahead_mode(const ngt_amd_index* ix, const SearchArgs& a, const ng
   return mode;
 }
 
+// NGT_AMD_SCHED=0: every search one launch in query order
+static int sched_mode() {
+  const char* v = getenv("NGT_AMD_SCHED");
+  return v ? atoi(v) : 1;
+}
+
+static uint32_t __float_as_uint_host(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+
+// the finished earlier launch's mean expansions per query, into the table
+static void sched_collect(SearchCtx* c) {
+  if (!c->stat_pending || hipEventQuery(c->ev_stat) != hipSuccess) return;
+  c->stat_pending = false;
+  if (c->h_stat[1] == 0) return;
+  const double mean = (double)c->h_stat[0] / (double)c->h_stat[1];
+  for (auto& m : c->sched_mean)
+    if (m.first == c->stat_key) {
+      m.second = mean;
+      return;
+    }
+  if (c->sched_mean.size() >= 64) c->sched_mean.erase(c->sched_mean.begin());
+  c->sched_mean.push_back({c->stat_key, mean});
+}
+
 static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_params* prm, const void* d_queries,
                       uint64_t query_bytes, uint32_t nq, const uint32_t* d_seeds,
                       const uint64_t* d_seed_off, uint32_t* d_ids, float* d_dists, uint32_t* d_n,
@@ -699,20 +726,98 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   a.spill = c->spill.p;
   a.spill_cap = ix->spill_cap;
   a.work = c->work.p;
-  HIP_OK(hipMemsetAsync(c->work.p, 0, sizeof(uint32_t), s));
+  HIP_OK(hipMemsetAsync(c->work.p, 0, 3 * sizeof(uint32_t), s));
   uint32_t slots = std::min<uint32_t>(c->slots, nq);
   c->launch_slots = slots;
   c->launch_la = la_mode;
+  // ---- launch schedule: "probe and resume" ------------------------------
+  // A launch's time is its slowest slot's: with ~2.4 queries per slot, a long
+  // search that happens to start last decides it (C2: 22.1 ms in query order,
+  // 16.6 ms longest-first with the true costs, profiles/r4d).  Cheap query
+  // features do not predict the cost (centroid distance, sampled distance
+  // contrast: rank correlation < 0.1); the search's own state does: the
+  // unchecked keys within the exploration radius after part of the search.
+  // So a probe launch runs every query for B expansions (B = 0.12 x the mean
+  // expansions per query of earlier launches of this configuration) and
+  // pauses the unfinished ones with their state saved; a one-workgroup
+  // counting sort orders them by that count; a resume launch continues them
+  // in that order.  Accepted-only visited sets only (the resume rebuilds the
+  // set from the popped ids and the unchecked keys; search_kernels.hip), so
+  // the results, distance bits and expansion counts are the single
+  // launch's.  Measured (profiles/r4e, r4f): C2 22.2 -> 18.6 ms per 10k-query
+  // search at 0.12 (19.4 at 0.25, 20.2 at 0.4).  The lookahead kernel (the
+  // ANNG's short lists) took the same scheme and ran slower at every
+  // fraction (0.08-0.5: 164-174 ms against 156), so it is not scheduled.
+  const bool sched_shape = !lat && la_mode < 0 && a.accepted_only && a.ht_log2 == 0 && a.vf_log2 != 0 && a.adj &&
+                           a.fcodes && a.k <= 64;
+  uint32_t budget = 0;
+  uint64_t skey = 0;
+  if (sched_shape && sched_mode() != 0) {
+    skey = (uint64_t)a.edge_size * 0x9E3779B97F4A7C15ull ^ ((uint64_t)__float_as_uint_host(a.coef) << 17) ^
+           ((uint64_t)a.k << 49) ^ (ix->rows_version * 0xC2B2AE3D27D4EB4Full) ^ (ix->adj_version << 7) ^
+           ((uint64_t)a.cq_cap << 33);
+    sched_collect(c);
+    double mean = 0.0;
+    for (auto& m : c->sched_mean)
+      if (m.first == skey) mean = m.second;
+    static const double frac = [] {
+      const char* v = getenv("NGT_AMD_SCHED_FRAC");
+      return v ? std::max(0.01, std::min(0.9, atof(v))) : 0.12;
+    }();
+    // test knob: a fixed budget for every eligible launch
+    const int forced = getenv("NGT_AMD_SCHED_B") ? std::max(0, atoi(getenv("NGT_AMD_SCHED_B"))) : 0;
+    if (forced) budget = (uint32_t)forced;
+    else if (mean > 0.0) budget = (uint32_t)std::max(8.0, mean * frac);
+    // a tail needs more queries than slots (forced: any launch, for tests)
+    if (!forced && (uint64_t)nq * 4 < (uint64_t)slots * 5) budget = 0;
+  }
+  c->launch_budget = budget;
+  if (sched_shape) {
+    HIP_OK(c->stat.alloc(2));
+    HIP_OK(hipMemsetAsync(c->stat.p, 0, 2 * sizeof(unsigned long long), s));
+    a.stat = c->stat.p;
+  }
   HIP_OK(hipEventRecord(c->ev0, s));
   if (lat) {
     HIP_OK(launch_graph_search_lat(a, slots, s));
   } else if (la_mode >= 0) {
     // full visited set unless the caller asked for the accepted-only one
     HIP_OK(launch_graph_search_la(a, la_mode, !a.accepted_only, slots, s));
+  } else if (budget) {
+    const PauseLayout lay(a.k, a.cq_cap, budget);
+    HIP_OK(c->qstate.alloc((size_t)nq * lay.total));
+    HIP_OK(c->qflag.alloc(nq));
+    HIP_OK(c->prio.alloc(nq));
+    HIP_OK(c->order.alloc(nq));
+    HIP_OK(hipMemsetAsync(c->qflag.p, 0, (size_t)nq * sizeof(uint32_t), s));
+    SearchArgs p = a;
+    p.pause_after = budget;
+    p.qstate = c->qstate.p;
+    p.qstate_stride = lay.total;
+    p.qflag = c->qflag.p;
+    p.prio = c->prio.p;
+    auto go = [&](const SearchArgs& x) -> hipError_t { return launch_graph_search(x, ix->metric, ix->otype, slots, s); };
+    HIP_OK(go(p));
+    HIP_OK(launch_schedule(c->qflag.p, c->prio.p, nq, c->order.p, c->work.p + 2, s));
+    SearchArgs r = p;
+    r.pause_after = 0;
+    r.order = c->order.p;
+    r.nwork_dev = c->work.p + 2;
+    r.work = c->work.p + 1;
+    HIP_OK(go(r));
   } else {
     HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
   }
   HIP_OK(hipEventRecord(c->ev1, s));
+  if (sched_shape) {
+    // this launch's mean expansions per query, for the next launch's budget
+    if (!c->h_stat) HIP_OK(hipHostMalloc((void**)&c->h_stat, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+    if (!c->ev_stat) HIP_OK(hipEventCreateWithFlags(&c->ev_stat, hipEventDisableTiming));
+    HIP_OK(hipMemcpyAsync(c->h_stat, c->stat.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(c->ev_stat, s));
+    c->stat_pending = true;
+    c->stat_key = skey;
+  }
   return 0;
 }
 
@@ -820,6 +925,12 @@ extern "C" int ngt_amd_last_search_lookahead(const ngt_amd_index* ix) {
   if (!ix) return -1;
   SearchCtx* c = ix->last_ctx.load();
   return c ? c->launch_la : -1;
+}
+
+extern "C" uint32_t ngt_amd_last_search_budget(const ngt_amd_index* ix) {
+  if (!ix) return 0;
+  SearchCtx* c = ix->last_ctx.load();
+  return c ? c->launch_budget : 0;
 }
 
 extern "C" uint32_t ngt_amd_last_search_slots(const ngt_amd_index* ix) {

@@ -95,6 +95,49 @@ struct SearchArgs {
   // latency kernel (search_lat.hip): speculation slots and LDS tail keys
   uint32_t lat_slots;
   uint32_t lat_tail;
+  // launch schedule (ngt_amd_api.cpp run_search, "probe and resume"): the
+  // w-th work item a slot claims is query order[w] (null: w), and a launch
+  // has *nwork_dev work items (null: nq).  A probe launch (pause_after > 0)
+  // pauses every query after pause_after expansions: its state goes to
+  // qstate[qi] (PauseLayout), qflag[qi] = 1 and prio[qi] = the unchecked keys
+  // within the exploration radius (the predicted rest of its search); a query
+  // that ends first writes its results and qflag[qi] = 2.  A later launch
+  // resumes the paused queries (qflag 1) from their saved state, longest
+  // predicted first.  Results are the same in any order and split.
+  const uint32_t* order;
+  const uint32_t* nwork_dev;
+  uint32_t pause_after;
+  uint8_t* qstate;
+  uint64_t qstate_stride;
+  uint32_t* qflag;
+  float* prio;
+  unsigned long long* stat;      // [2]: expansions and queries finished by this launch (device sums) or null
+};
+
+// One paused query's saved state (the one-expansion kernel's accepted-only
+// filtered path): counters and radius, the results, the unchecked keys (LDS
+// and spill) and the ids popped so far.  The accepted-only visited set is
+// rebuilt from the popped ids and the unchecked keys: every accepted id is
+// one of them, except keys compaction dropped beyond the exploration radius,
+// which a re-evaluation rejects again (search_common.h not_accepted).
+constexpr uint32_t kPauseSpillMax = 1024;  // a query with more spill keys is not paused
+constexpr uint32_t kPauseStepMax = 8;      // popped ids one step may add past pause_after
+struct PauseHdr {
+  uint32_t ncq, nspill, nres, npop, maxq, pad0;
+  float radius, pad1;
+  unsigned long long ndist, nvisit, nexp, nedge, nexact, pad2;
+};
+struct PauseLayout {
+  uint64_t off_res, off_cq, off_spill, off_pop, total;
+  __host__ __device__ PauseLayout(uint32_t k, uint32_t cq_cap, uint32_t pause_after) {
+    off_res = 128;
+    off_cq = off_res + 8ull * ((k + 1) & ~1u);
+    off_spill = off_cq + 8ull * cq_cap;
+    off_pop = off_spill + 8ull * kPauseSpillMax;
+    // a lookahead step commits up to kPauseStepMax targets, so a query may
+    // pass pause_after by that many before the check at the step's start
+    total = (off_pop + 4ull * (pause_after + kPauseStepMax) + 127) & ~127ull;
+  }
 };
 
 // Serving form of the latency kernel (search_lat.hip, serve.cpp): a resident
@@ -278,6 +321,9 @@ hipError_t launch_pack_results(const uint32_t* ids, const float* dists, const ui
 hipError_t launch_merge_packed(const MergeArgs& a, const uint64_t* packed, hipStream_t s);
 hipError_t launch_tree_seeds(const TreeSeedArgs& a, int metric, int otype, hipStream_t s);
 size_t search_lds_bytes(const SearchArgs& a, int otype);
+// the resume launch's order: paused queries (qflag 1) by descending prio
+hipError_t launch_schedule(const uint32_t* qflag, const float* prio, uint32_t nq, uint32_t* order, uint32_t* n_out,
+                           hipStream_t s);
 hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,
                                hipStream_t s);
 hipError_t launch_linear_search(const LinearArgs& a, int metric, int otype, uint32_t nslices,

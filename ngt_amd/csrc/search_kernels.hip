@@ -145,6 +145,63 @@ __device__ __forceinline__ void cq_chunk_min(const uint64_t* cq, uint64_t* cmin,
   if (lane_id() == 0) cmin[c] = m;
 }
 
+// Probe-and-resume schedule (SearchArgs::pause_after): a paused query's
+// state to and from its record (PauseLayout).
+__device__ __forceinline__ void pause_save(uint8_t* prec, const PauseLayout& play, const SearchState& st,
+                                          const uint64_t* spill, uint32_t ncq, uint32_t nspill, uint32_t nres,
+                                          float expr, float* prio, uint32_t* qflag) {
+  const int lane = lane_id();
+  uint64_t* rres = reinterpret_cast<uint64_t*>(prec + play.off_res);
+  uint64_t* rcq = reinterpret_cast<uint64_t*>(prec + play.off_cq);
+  uint64_t* rsp = reinterpret_cast<uint64_t*>(prec + play.off_spill);
+  for (uint32_t i = lane; i < nres; i += 64) rres[i] = st.res[i];
+  uint32_t live = 0;
+  for (uint32_t i = lane; i < ncq; i += 64) {
+    const uint64_t key = st.cq[i];
+    rcq[i] = key;
+    live += key_dist(key) <= expr ? 1u : 0u;
+  }
+  for (uint32_t i = lane; i < nspill; i += 64) {
+    const uint64_t key = spill[i];
+    rsp[i] = key;
+    live += key_dist(key) <= expr ? 1u : 0u;
+  }
+  // the predicted rest of the search: unchecked keys within the exploration radius
+  live = wave_sum_u32(live);
+  if (lane == 0) {
+    *prio = (float)live;
+    *qflag = 1u;
+  }
+}
+
+__device__ __forceinline__ void pause_restore(const uint8_t* prec, const PauseLayout& play, SearchState& st,
+                                           uint64_t* spill, uint8_t* vis, uint32_t epoch, PauseHdr& hv) {
+  const int lane = lane_id();
+  hv = *reinterpret_cast<const PauseHdr*>(prec);
+  const uint64_t* rres = reinterpret_cast<const uint64_t*>(prec + play.off_res);
+  const uint64_t* rcq = reinterpret_cast<const uint64_t*>(prec + play.off_cq);
+  const uint64_t* rsp = reinterpret_cast<const uint64_t*>(prec + play.off_spill);
+  const uint32_t* rpop = reinterpret_cast<const uint32_t*>(prec + play.off_pop);
+  auto remark = [&](uint32_t id) {
+    const uint32_t b = (id * 0x85EBCA77u) >> st.vf_shift;
+    atomicOr(st.vf + (b >> 5), 1u << (b & 31));
+    vis[id] = (uint8_t)epoch;
+  };
+  for (uint32_t i = lane; i < hv.nres; i += 64) st.res[i] = rres[i];
+  for (uint32_t i = lane; i < hv.ncq; i += 64) {
+    const uint64_t key = rcq[i];
+    st.cq[i] = key;
+    remark(key_id(key));
+  }
+  for (uint32_t i = lane; i < hv.nspill; i += 64) {
+    const uint64_t key = rsp[i];
+    spill[i] = key;
+    remark(key_id(key));
+  }
+  for (uint32_t i = lane; i < hv.npop; i += 64) remark(rpop[i]);
+  __syncthreads();
+}
+
 template <int M, typename T, int NCH, int G>
 __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -198,11 +255,16 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   const uint32_t hcap = use_hash ? 1u << a.ht_log2 : 0u;
   const uint32_t hlimit = hcap - (hcap >> 2);  // 75 % load factor
 
+  // launch schedule (SearchArgs::order / nwork_dev / pause_after)
+  const uint32_t nwork = a.nwork_dev ? *a.nwork_dev : a.nq;
   for (;;) {
-    uint32_t qi = 0;
-    if (lane == 0) qi = atomicAdd(a.work, 1u);
-    qi = __shfl(qi, 0, 64);
-    if (qi >= a.nq) break;
+    uint32_t w = 0;
+    if (lane == 0) w = atomicAdd(a.work, 1u);
+    w = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+    if (w >= nwork) break;
+    const uint32_t qi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(a.order ? a.order[w] : w));
+    // a query the probe launch paused: its saved state, not the seeds
+    const bool resume = a.qflag != nullptr && __builtin_amdgcn_readfirstlane((int)a.qflag[qi]) == 1;
 
     // ---- per-query init -----------------------------------------------
     for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
@@ -256,7 +318,26 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     // ---- setupDistances + setupSeeds (Graph.cpp:293-367) ----------------
     const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
     const uint32_t ns = a.seed_off ? (uint32_t)(a.seed_off[qi + 1] - sb) : a.seed_count[qi];
-    for (uint32_t base = 0; base < ns; base += 64) {
+    if (resume) {
+      // the paused query's state: counters, results, unchecked keys (LDS and
+      // this slot's spill), and its accepted-only visited set rebuilt from
+      // the popped ids and the unchecked keys in this slot's new epoch
+      PauseHdr h;
+      pause_restore(a.qstate + (uint64_t)qi * a.qstate_stride, PauseLayout(a.k, a.cq_cap, 0), st, spill, vis, epoch,
+                    h);
+      ncq = h.ncq;
+      nspill = h.nspill;
+      nres = h.nres;
+      maxq = h.maxq;
+      ndist = h.ndist;
+      nvisit = h.nvisit;
+      nexp = h.nexp;
+      nedge = h.nedge;
+      nexact = h.nexact;
+      for (uint32_t c = 0; c < ((ncq + 63) >> 6); c++) cq_chunk_min(st.cq, cmin, ncq, c);
+      __syncthreads();
+    }
+    for (uint32_t base = 0; base < (resume ? 0u : ns); base += 64) {
       const uint32_t m = ns - base < 64 ? ns - base : 64;
       if ((uint32_t)lane < m) st.nid[lane] = a.seeds[sb + base + lane];
       __syncthreads();
@@ -354,8 +435,17 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     (void)pf_node; (void)pf0; (void)pf1; (void)pf2; (void)pf3;
 
     // ---- best-first loop (Graph.cpp:430-486) ----------------------------
+    bool paused = false;
     for (;;) {
       NGT_MARK(t_rest);
+      // probe launch: stop here; the state is saved after the loop
+      // (only while the popped-id log is complete: a query whose spill held
+      // it past the budget runs to its end)
+      if (a.pause_after && nexp >= a.pause_after && nexp <= a.pause_after + kPauseStepMax &&
+          nspill <= kPauseSpillMax) {
+        paused = true;
+        break;
+      }
       // pop the minimum key
       // best chunk minimum (<= 128 chunks: two per lane), then the spill
       uint64_t best = ~0ull;
@@ -405,6 +495,10 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       NGT_MARK(t_pop);
 
       const uint32_t target = key_id(wbest);
+      // probe launch: the popped ids (the accepted-only visited set of a resume)
+      if (a.pause_after && lane == 0 && nexp <= a.pause_after + kPauseStepMax)
+        reinterpret_cast<uint32_t*>(a.qstate + (uint64_t)qi * a.qstate_stride +
+                                    PauseLayout(a.k, a.cq_cap, 0).off_pop)[nexp - 1] = target;
       // adjacency: padded fixed-stride rows (one load, 0-terminated) or CSR
       uint64_t eb, deg;
       const bool padded = a.adj != nullptr;
@@ -560,6 +654,28 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       }
     }
 
+    if (paused) {
+      // save the state, predict the rest of the search by the unchecked keys
+      // within the exploration radius, and take the next query
+      uint8_t* prec = a.qstate + (uint64_t)qi * a.qstate_stride;
+      if (lane == 0) {
+        PauseHdr* h = reinterpret_cast<PauseHdr*>(prec);
+        h->ncq = ncq;
+        h->nspill = nspill;
+        h->nres = nres;
+        h->npop = (uint32_t)nexp;
+        h->maxq = maxq;
+        h->ndist = ndist;
+        h->nvisit = nvisit;
+        h->nexp = nexp;
+        h->nedge = nedge;
+        h->nexact = nexact;
+      }
+      pause_save(prec, PauseLayout(a.k, a.cq_cap, 0), st, spill, ncq, nspill, nres, expr, a.prio + qi,
+                 a.qflag + qi);
+      __syncthreads();
+      continue;
+    }
     // ---- results (moveFrom: ascending (distance, id), ObjectSpace.h:49-57)
     for (uint32_t i = lane; i < nres; i += 64) {
       a.out_ids[(uint64_t)qi * a.k + i] = key_id(st.res[i]);
@@ -567,6 +683,11 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     }
     if (lane == 0) {
       a.out_n[qi] = nres;
+      if (a.qflag) a.qflag[qi] = 2u;
+      if (a.stat) {
+        atomicAdd(a.stat, (unsigned long long)nexp);
+        atomicAdd(a.stat + 1, 1ull);
+      }
       if (a.counters) {
         uint64_t* c = a.counters + (uint64_t)qi * 8;
         c[0] = ndist;
@@ -826,6 +947,55 @@ size_t search_lds_bytes(const SearchArgs& a, int otype) {
   b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
   if (a.fcodes) b += (size_t)a.dp + 256;  // the query's filter bytes and the pending survivors
   return b;
+}
+
+// Launch schedule of the resume launch: the queries the probe launch paused
+// (qflag 1), in descending predicted rest of their search (prio: unchecked
+// keys within the exploration radius), as a counting sort over 1024
+// logarithmic buckets in one workgroup; *n_out = their count.  The order
+// inside a bucket is whatever the atomics give: any order gives the same
+// results, the schedule only decides when each query runs.
+__global__ void __launch_bounds__(1024) ngt_schedule_kernel(const uint32_t* qflag, const float* prio, uint32_t nq,
+                                                           uint32_t* order, uint32_t* n_out) {
+  constexpr uint32_t NB = 1024;
+  __shared__ uint32_t hist[NB];
+  __shared__ uint32_t part[NB / 64];
+  const uint32_t t = threadIdx.x;
+  hist[t] = 0u;
+  __syncthreads();
+  auto bucket = [&](uint32_t q) -> uint32_t {
+    const float p = prio[q];
+    const float l = __log2f(1.0f + (p > 0.0f ? p : 0.0f)) * 48.0f;
+    const uint32_t b = l < (float)(NB - 1) ? (uint32_t)l : NB - 1;
+    return NB - 1 - b;  // descending
+  };
+  for (uint32_t q = t; q < nq; q += NB)
+    if (qflag[q] == 1u) atomicAdd(hist + bucket(q), 1u);
+  __syncthreads();
+  // exclusive prefix over the buckets: per wave of 64, then over the 16 waves
+  const uint32_t lane = t & 63, wv = t >> 6;
+  const uint32_t v = hist[t];
+  uint32_t incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+    if ((int)lane >= o) incl += u;
+  }
+  if (lane == 63) part[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t i = 0; i < wv; i++) base += part[i];
+  __syncthreads();
+  hist[t] = base + incl - v;  // the bucket's first position
+  if (t == NB - 1) *n_out = base + incl;
+  __syncthreads();
+  for (uint32_t q = t; q < nq; q += NB)
+    if (qflag[q] == 1u) order[atomicAdd(hist + bucket(q), 1u)] = q;
+}
+
+hipError_t launch_schedule(const uint32_t* qflag, const float* prio, uint32_t nq, uint32_t* order, uint32_t* n_out,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(ngt_schedule_kernel, dim3(1), dim3(1024), 0, s, qflag, prio, nq, order, n_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,

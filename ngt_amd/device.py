@@ -178,6 +178,12 @@ class DeviceIndex(object):
         0 lookahead with a wave per query, 1 lookahead with eight waves per query."""
         return int(self.L.ngt_amd_last_search_lookahead(self.h))
 
+    def last_search_budget(self):
+        """0: the last search ran as one launch in query order; B > 0: probe
+        launch (every query paused after B expansions) + resume launch,
+        longest predicted first (ngt_amd_last_search_budget)."""
+        return int(self.L.ngt_amd_last_search_budget(self.h))
+
     def last_search_slots(self):
         """Workgroups (resident query slots) of the last search launch."""
         return int(self.L.ngt_amd_last_search_slots(self.h))
