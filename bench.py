@@ -530,6 +530,7 @@ def main():
         torch.cuda.synchronize()
         kms.append(ix.last_search_kernel_ms())
     filtered = (not qgm) and ix.last_search_filtered()
+    budget = 0 if qgm else ix.last_search_budget()
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -728,7 +729,12 @@ def main():
                          # (a single launch's last round of queries leaves the GPU part-empty)
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
                          "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
-                         "bytes_split": split},
+                         "bytes_split": split,
+                         # the probe-and-resume schedule: one search = a probe dispatch (every query
+                         # paused after `budget` expansions) + a resume dispatch, longest predicted first;
+                         # kernel_ms spans both (ngt_amd_api.cpp run_search)
+                         "search_dispatches": 2 if budget else 1,
+                         "schedule_budget": budget},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "sweep": sweep,
@@ -1321,7 +1327,12 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
                          "what": "one shard's search launch alone (mean over the %d local shards)" % S,
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
                          "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
-                         "bytes_split": split},
+                         "bytes_split": split,
+                         # the probe-and-resume schedule: one search = a probe dispatch (every query
+                         # paused after `budget` expansions) + a resume dispatch, longest predicted first;
+                         # kernel_ms spans both (ngt_amd_api.cpp run_search)
+                         "search_dispatches": 2 if budget else 1,
+                         "schedule_budget": budget},
             "cpu_baseline": cpu, "parity_sample": parity, "sweep": sweep}
         if qgm:
             line["config"]["result_expansion"] = args.expansion

@@ -6,7 +6,9 @@
 # hits/misses and the L2 memory-side read requests (all of them, and those
 # destined for DRAM -- Infinity-Cache hits included: no TCC counter separates
 # them).
-#   scripts/pmc_r4.sh <outdir> <name> <bench args...>
+#   [PMC_LAST=N] scripts/pmc_r4.sh <outdir> <name> <bench args...>
+# (PMC_LAST: count only each kernel's last N dispatches -- the --pmc-launches
+# searches; a scheduled search is two dispatches, probe and resume)
 # writes <outdir>/<name>_{trace,fetch,write,sq,tcc}{.json,.log,_pmc.json} and the
 # trace's kernel_stats.csv.
 set -o pipefail
@@ -25,6 +27,6 @@ for pass in fetch write sq tcc; do
   case $pass in fetch) C="FETCH_SIZE";; write) C="WRITE_SIZE";; sq) C="$SQ";; tcc) C="$TCC";; esac
   timeout -k 10 400 rocprofv3 --pmc $C -d "$R/$out/${name}_$pass" -o $pass --output-format csv -- \
     python3 "$R/bench.py" "$@" > "$R/$out/${name}_$pass.json" 2> "$R/$out/${name}_$pass.log" || exit 1
-  python3 "$R/scripts/pmc_summary.py" "$R/$out" "${name}_$pass" > /dev/null || exit 1
+  python3 "$R/scripts/pmc_summary.py" "$R/$out" "${name}_$pass" --last ${PMC_LAST:-0} > /dev/null || exit 1
 done
 echo "pmc $name done"

@@ -36,6 +36,10 @@ _, wr = pick("write")
 _, sq = pick("sq")
 n = fe["dispatches"]
 assert wr["dispatches"] == n and sq["dispatches"] == n
+# a search may be several dispatches of the kernel (the probe-and-resume
+# schedule: 2); figures are per search
+dps = int(key.pop("dispatches_per_search", 1))
+n = n / dps
 fetch = fe["FETCH_SIZE"] / n * 1024 * 2
 write = wr["WRITE_SIZE"] / n * 1024
 per = {c: v / n for c, v in sq.items() if c.startswith("SQ_")}
@@ -44,7 +48,7 @@ if os.path.exists(os.path.join(d, "%s_tcc_pmc.json" % name)):
     # L2 hit rate and the share of L2 memory-side read requests destined for
     # DRAM (the Infinity Cache sits behind that interface: its hits count)
     _, tc = pick("tcc")
-    assert tc["dispatches"] == n
+    assert tc["dispatches"] == round(n * dps)
     tcc = {c: v / n for c, v in tc.items() if c.startswith("TCC_")}
     per.update(tcc)
 avg_ns = None
@@ -52,15 +56,25 @@ with open(os.path.join(d, name + "_kernel_stats.csv")) as f:
     for row in csv.DictReader(f):
         if ksub in row["Name"]:
             avg_ns = float(row["AverageNs"])
+search_ns = None
+tpath = os.path.join(d, name + "_kernel_trace.csv")
+if dps > 1 and os.path.exists(tpath):
+    # per search: the last searches' dispatches in the trace, summed per search
+    with open(tpath) as f:
+        rs = [r for r in csv.DictReader(f) if ksub in r["Kernel_Name"]]
+    rs.sort(key=lambda r: int(r["Dispatch_Id"]))
+    last = rs[-int(round(n * dps)):]
+    search_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last) / n
 e = dict(key)
 e.update({"kernel": kname.replace("void ngt_amd::", ""), "fetch_bytes": fetch, "write_bytes": write,
           "traffic_bytes": fetch + write, "counters_per_launch": per,
-          "trace_avg_kernel_ms": avg_ns / 1e6 if avg_ns else None,
-          "source": "%s/%s_{fetch,write,sq}_pmc.json, %s_kernel_stats.csv (scripts/pmc_r3.sh: rocprofv3 "
+          "trace_avg_kernel_ms": (search_ns if search_ns else avg_ns) / 1e6 if avg_ns else None,
+          "dispatches_per_search": dps,
+          "source": "%s/%s_{fetch,write,sq}_pmc.json, %s_kernel_stats.csv (scripts/pmc_r4.sh: rocprofv3 "
                     "--kernel-trace --stats, then separate --pmc passes FETCH_SIZE | WRITE_SIZE | %s%s; %d dispatches "
-                    "of the timed configuration each; FETCH_SIZE x1024 x2, WRITE_SIZE x1024)" % (
+                    "of the timed configuration each, %d per search; FETCH_SIZE x1024 x2, WRITE_SIZE x1024)" % (
                         d, name, name, " ".join(sorted(c for c in per if c.startswith("SQ_"))),
-                        (" | " + " ".join(sorted(tcc))) if tcc else "", n)})
+                        (" | " + " ".join(sorted(tcc))) if tcc else "", round(n * dps), dps)})
 if tcc:
     e["l2_hit_rate"] = tcc["TCC_HIT_sum"] / max(1.0, tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"])
     e["dram_destined_read_frac"] = tcc["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, tcc["TCC_EA0_RDREQ_sum"])
