@@ -326,7 +326,13 @@ def main():
         # construction, ngt_save_index), checked against the reference's own
         # build of the same data (tests/golden/c2_anng_ref.json), and searched
         # on the device index that handle serves (ngt_get_device_index)
-        ix, offsets, edges, tree, build_s, anng_check, cx = build_anng_capi(args, torch, dev, base, N, D, es_prop)
+        if N > 2_000_000:
+            # an index too large to write in the reference's format per run:
+            # the same device construction, driven in id ranges with progress
+            ix, offsets, edges, tree, build_s, anng_check, cx = build_anng_device(args, torch, dev, rows, N, D,
+                                                                                 es_prop, local)
+        else:
+            ix, offsets, edges, tree, build_s, anng_check, cx = build_anng_capi(args, torch, dev, base, N, D, es_prop)
     else:
         ix = DeviceIndex(metric, "float", D, device=local)
         ix.set_objects_device(rows.data_ptr(), N + 1)
@@ -671,7 +677,11 @@ def main():
         ref_check = reference_fixture_check(ix, qdev, dp, K, dev, torch)
 
     if rank == 0:
-        if args.mode == "exact" and not c3:
+        if args.mode == "exact" and not c3 and N > 2_000_000:
+            metric_name = "QPS at recall@10=0.95, %d x %d-d float L2 on one GPU (C4's index as one graph)" % (N, D)
+            workload = ("C4 on one GPU: %d x %d float L2, ONE device-built ANNG over all objects (not shards), "
+                        "%d queries/step, k=%d" % (N, D, NQ, K))
+        elif args.mode == "exact" and not c3:
             metric_name = HEADLINE
             workload = "C2: %d x %d float L2 graph search, %d queries/step/GPU, k=%d" % (N, D, NQ, K)
         elif args.mode == "exact":
@@ -875,6 +885,40 @@ def sha256_file(path):
         for b in iter(lambda: f.read(1 << 24), b""):
             h.update(b)
     return h.hexdigest()
+
+
+def build_anng_device(args, torch, dev, rows, N, D, es_prop, local):
+    """GraphAndTreeIndex::createIndex (Index.cpp:1158-1257) of N HBM-resident
+    rows with this library's device construction (ngt_amd_build_begin /
+    _insert over id ranges, the path ngt_create_index takes), then the graph
+    and DVP tree installed for search on the same index."""
+    from ngt_amd.device import DeviceIndex
+    ix = DeviceIndex("l2", "float", D, device=local)
+    ix.set_objects_device(rows.data_ptr(), N + 1)
+    t0 = time.time()
+    step = 250_000
+    for first in range(1, N + 1, step):
+        if first == 1:
+            import ctypes as _ct
+            from ngt_amd._sigs import BuildParams
+            prm = BuildParams(args.anng_edges, es_prop, 200, args.seed_size, 0.1, 0)
+            if ix.L.ngt_amd_build_begin(ix.h, _ct.byref(prm)) != 0:
+                raise SystemExit("bench: ngt_amd_build_begin failed")
+        if ix.L.ngt_amd_build_insert(ix.h, first, min(N + 1, first + step)) != 0:
+            from ngt_amd import lib
+            raise SystemExit("bench: device construction failed: " + lib().ngt_amd_last_error().decode())
+        log("ANNG construction: %d of %d objects inserted (%.0f s)" % (min(N, first + step - 1), N, time.time() - t0))
+    build_s = time.time() - t0
+    offs, ids, _ = ix.build_graph()
+    tree = ix.build_tree()
+    ix.set_graph(offs, ids)
+    ix.set_tree(tree)
+    ix.set_search_property(es_prop, 30, 20, args.seed_size, 0)
+    log("ANNG (E=%d) of %d objects built on the device in %.1f s; %d edges, mean degree %.1f" % (
+        args.anng_edges, N, build_s, len(ids), len(ids) / N))
+    offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    edges = torch.from_numpy(ids.astype(np.int32)).to(dev)
+    return ix, offsets, edges, tree, build_s, {"reference": None, "built": "device, ngt_amd_build_insert in id ranges"}, None
 
 
 def build_anng_capi(args, torch, dev, data, N, D, es_prop):

@@ -1,0 +1,8 @@
+#!/bin/bash
+# C4's 10M x 128 as ONE device-built ANNG on one GPU (not 8 sub-shards): build
+# in id ranges (progress every 250k objects), tree seeds, prf edge size 40
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r4l}; mkdir -p $O
+timeout -k 10 1080 python -u bench.py --graph anng --n ${N:-10000000} --steps 3 --warmup 1 --cpu-seconds 10 --latency-queries 0 \
+  --anng-line off > $O/c4_onegraph.json 2> $O/c4_onegraph.log || { tail -20 $O/c4_onegraph.log; exit 1; }
+python3 -c "import json; d=json.load(open('$O/c4_onegraph.json')); print('c4', round(d['value']), d['config']['recall_at_10'], round(d['roofline']['kernel_ms'],1), round(d['roofline']['frac'],3), d['config'].get('graph_build_s'), (d.get('parity_sample') or {}).get('identical'))"
