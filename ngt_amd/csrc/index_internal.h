@@ -110,11 +110,12 @@ struct SearchCtx {
   DevBuf<float> ivf_cd;
   DevBuf<int> err;               // device error flag of the launches on this stream
   // launch schedule ("probe and resume", ngt_amd_api.cpp run_search): the
-  // paused queries' states, the schedule's counters and priority buckets; the
+  // paused queries' states, flags, predictions and the resume order; the
   // mean expansions per query of earlier launches of the same configuration
   // (a pinned copy of the device sums, read once the launch has finished)
   DevBuf<uint8_t> qstate;
-  DevBuf<uint32_t> sched, sched_items;
+  DevBuf<uint32_t> qflag, order;
+  DevBuf<float> prio;
   DevBuf<unsigned long long> stat;
   unsigned long long* h_stat = nullptr;
   hipEvent_t ev_stat = nullptr;

@@ -786,17 +786,25 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   } else if (budget) {
     const PauseLayout lay(a.k, a.cq_cap, budget);
     HIP_OK(c->qstate.alloc((size_t)nq * lay.total));
-    HIP_OK(c->sched.alloc(2 + 2 * kSchedBuckets));
-    HIP_OK(c->sched_items.alloc((size_t)kSchedBuckets * nq));
-    HIP_OK(hipMemsetAsync(c->sched.p, 0, (2 + 2 * kSchedBuckets) * sizeof(uint32_t), s));
-    HIP_OK(hipMemsetAsync(c->sched_items.p, 0, (size_t)kSchedBuckets * nq * sizeof(uint32_t), s));
+    HIP_OK(c->qflag.alloc(nq));
+    HIP_OK(c->prio.alloc(nq));
+    HIP_OK(c->order.alloc(nq));
+    HIP_OK(hipMemsetAsync(c->qflag.p, 0, (size_t)nq * sizeof(uint32_t), s));
     SearchArgs p = a;
     p.pause_after = budget;
     p.qstate = c->qstate.p;
     p.qstate_stride = lay.total;
-    p.sched = c->sched.p;
-    p.sched_items = c->sched_items.p;
-    HIP_OK(launch_graph_search(p, ix->metric, ix->otype, slots, s));
+    p.qflag = c->qflag.p;
+    p.prio = c->prio.p;
+    auto go = [&](const SearchArgs& x) -> hipError_t { return launch_graph_search(x, ix->metric, ix->otype, slots, s); };
+    HIP_OK(go(p));
+    HIP_OK(launch_schedule(c->qflag.p, c->prio.p, nq, c->order.p, c->work.p + 2, s));
+    SearchArgs r = p;
+    r.pause_after = 0;
+    r.order = c->order.p;
+    r.nwork_dev = c->work.p + 2;
+    r.work = c->work.p + 1;
+    HIP_OK(go(r));
   } else {
     HIP_OK(launch_graph_search(a, ix->metric, ix->otype, slots, s));
   }

@@ -147,9 +147,9 @@ __device__ __forceinline__ void cq_chunk_min(const uint64_t* cq, uint64_t* cmin,
 
 // Probe-and-resume schedule (SearchArgs::pause_after): a paused query's
 // state to and from its record (PauseLayout).
-__device__ __forceinline__ uint32_t pause_save(uint8_t* prec, const PauseLayout& play, const SearchState& st,
-                                              const uint64_t* spill, uint32_t ncq, uint32_t nspill, uint32_t nres,
-                                              float expr) {
+__device__ __forceinline__ void pause_save(uint8_t* prec, const PauseLayout& play, const SearchState& st,
+                                          const uint64_t* spill, uint32_t ncq, uint32_t nspill, uint32_t nres,
+                                          float expr, float* prio, uint32_t* qflag) {
   const int lane = lane_id();
   uint64_t* rres = reinterpret_cast<uint64_t*>(prec + play.off_res);
   uint64_t* rcq = reinterpret_cast<uint64_t*>(prec + play.off_cq);
@@ -167,54 +167,10 @@ __device__ __forceinline__ uint32_t pause_save(uint8_t* prec, const PauseLayout&
     live += key_dist(key) <= expr ? 1u : 0u;
   }
   // the predicted rest of the search: unchecked keys within the exploration radius
-  return wave_sum_u32(live);
-}
-
-// The next query of a scheduled launch (SearchArgs::sched): a fresh one while
-// any is left, else the paused one with the longest predicted rest (the
-// highest non-empty bucket, one bucket per lane); ~0 once every query has
-// finished.  Every wait is for a push another slot has already counted, or for
-// a query in flight to pause or finish, so the loop ends.
-__device__ uint32_t sched_next(const SearchArgs& a, bool& resume) {
-  const int lane = lane_id();
-  resume = false;
-  uint32_t* pushc = a.sched + 2;
-  uint32_t* popc = a.sched + 2 + kSchedBuckets;
-  for (;;) {
-    uint32_t w = ~0u;
-    if (lane == 0 && __hip_atomic_load(a.sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.nq)
-      w = atomicAdd(a.sched, 1u);
-    w = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
-    if (w < a.nq) return w;
-    const uint32_t pn = __hip_atomic_load(pushc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t cn = __hip_atomic_load(popc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t ne = ballot64(cn < pn);
-    if (ne) {
-      const int b = 63 - __builtin_clzll(ne);
-      uint32_t ok = 0, idx = 0;
-      if (lane == b) {
-        idx = cn;
-        ok = __hip_atomic_compare_exchange_strong(popc + b, &idx, cn + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
-        idx = cn;
-      }
-      if (!__builtin_amdgcn_readlane((int)ok, b)) continue;  // another slot took it: look again
-      idx = (uint32_t)__builtin_amdgcn_readlane((int)idx, b);
-      uint32_t item = 0;
-      if (lane == 0) {
-        // the pusher counted this entry before we saw it: its store is on the way
-        const uint32_t* slot = a.sched_items + (uint64_t)b * a.nq + idx;
-        while ((item = __hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      item = (uint32_t)__builtin_amdgcn_readfirstlane((int)item);
-      // the paused query's record, written on another CU (another XCD's L2)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      resume = true;
-      return item - 1u;
-    }
-    if (__hip_atomic_load(a.sched + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.nq) return ~0u;
-    __builtin_amdgcn_s_sleep(8);
+  live = wave_sum_u32(live);
+  if (lane == 0) {
+    *prio = (float)live;
+    *qflag = 1u;
   }
 }
 
@@ -299,20 +255,17 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
   const uint32_t hcap = use_hash ? 1u << a.ht_log2 : 0u;
   const uint32_t hlimit = hcap - (hcap >> 2);  // 75 % load factor
 
+  // launch schedule (SearchArgs::order / nwork_dev / pause_after)
+  const uint32_t nwork = a.nwork_dev ? *a.nwork_dev : a.nq;
   for (;;) {
-    uint32_t qi;
-    bool resume = false;
-    if (a.sched) {
-      // launch schedule (SearchArgs::sched): fresh queries, then the paused ones
-      qi = sched_next(a, resume);
-      if (qi == ~0u) break;
-    } else {
-      uint32_t w = 0;
-      if (lane == 0) w = atomicAdd(a.work, 1u);
-      w = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
-      if (w >= a.nq) break;
-      qi = w;
-    }
+    uint32_t w = 0;
+    if (lane == 0) w = atomicAdd(a.work, 1u);
+    w = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+    if (w >= nwork) break;
+    const uint32_t qi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(a.order ? a.order[w] : w));
+    // a query the probe launch paused: its saved state, not the seeds
+    const bool resume = a.qflag != nullptr && __builtin_amdgcn_readfirstlane((int)a.qflag[qi]) == 1;
+
     // ---- per-query init -----------------------------------------------
     for (uint32_t i = lane; i < hcap; i += 64) st.ht[i] = 0u;
     for (uint32_t i = lane; i < vf_words; i += 64) st.vf[i] = 0u;
@@ -488,7 +441,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
       // probe launch: stop here; the state is saved after the loop
       // (only while the popped-id log is complete: a query whose spill held
       // it past the budget runs to its end)
-      if (a.pause_after && !resume && nexp >= a.pause_after && nexp <= a.pause_after + kPauseStepMax &&
+      if (a.pause_after && nexp >= a.pause_after && nexp <= a.pause_after + kPauseStepMax &&
           nspill <= kPauseSpillMax) {
         paused = true;
         break;
@@ -543,7 +496,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
 
       const uint32_t target = key_id(wbest);
       // probe launch: the popped ids (the accepted-only visited set of a resume)
-      if (a.pause_after && !resume && lane == 0 && nexp <= a.pause_after + kPauseStepMax)
+      if (a.pause_after && lane == 0 && nexp <= a.pause_after + kPauseStepMax)
         reinterpret_cast<uint32_t*>(a.qstate + (uint64_t)qi * a.qstate_stride +
                                     PauseLayout(a.k, a.cq_cap, 0).off_pop)[nexp - 1] = target;
       // adjacency: padded fixed-stride rows (one load, 0-terminated) or CSR
@@ -718,16 +671,8 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         h->nedge = nedge;
         h->nexact = nexact;
       }
-      const uint32_t live = pause_save(prec, PauseLayout(a.k, a.cq_cap, 0), st, spill, ncq, nspill, nres, expr);
-      // the record, then its entry in the bucket of its predicted rest
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      if (lane == 0) {
-        const float l = __log2f(1.0f + (float)live) * 6.0f;
-        const uint32_t b = l < (float)(kSchedBuckets - 1) ? (uint32_t)l : kSchedBuckets - 1;
-        const uint32_t idx = atomicAdd(a.sched + 2 + b, 1u);
-        __hip_atomic_store(a.sched_items + (uint64_t)b * a.nq + idx, qi + 1u, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
+      pause_save(prec, PauseLayout(a.k, a.cq_cap, 0), st, spill, ncq, nspill, nres, expr, a.prio + qi,
+                 a.qflag + qi);
       __syncthreads();
       continue;
     }
@@ -738,7 +683,7 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
     }
     if (lane == 0) {
       a.out_n[qi] = nres;
-      if (a.sched) atomicAdd(a.sched + 1, 1u);  // finished (the scheduled launch's exit count)
+      if (a.qflag) a.qflag[qi] = 2u;
       if (a.stat) {
         atomicAdd(a.stat, (unsigned long long)nexp);
         atomicAdd(a.stat + 1, 1ull);
@@ -1002,6 +947,55 @@ size_t search_lds_bytes(const SearchArgs& a, int otype) {
   b += ((size_t)a.dp * (otype == kFloat ? 4 : 1) + 15) & ~(size_t)15;
   if (a.fcodes) b += (size_t)a.dp + 256;  // the query's filter bytes and the pending survivors
   return b;
+}
+
+// Launch schedule of the resume launch: the queries the probe launch paused
+// (qflag 1), in descending predicted rest of their search (prio: unchecked
+// keys within the exploration radius), as a counting sort over 1024
+// logarithmic buckets in one workgroup; *n_out = their count.  The order
+// inside a bucket is whatever the atomics give: any order gives the same
+// results, the schedule only decides when each query runs.
+__global__ void __launch_bounds__(1024) ngt_schedule_kernel(const uint32_t* qflag, const float* prio, uint32_t nq,
+                                                           uint32_t* order, uint32_t* n_out) {
+  constexpr uint32_t NB = 1024;
+  __shared__ uint32_t hist[NB];
+  __shared__ uint32_t part[NB / 64];
+  const uint32_t t = threadIdx.x;
+  hist[t] = 0u;
+  __syncthreads();
+  auto bucket = [&](uint32_t q) -> uint32_t {
+    const float p = prio[q];
+    const float l = __log2f(1.0f + (p > 0.0f ? p : 0.0f)) * 48.0f;
+    const uint32_t b = l < (float)(NB - 1) ? (uint32_t)l : NB - 1;
+    return NB - 1 - b;  // descending
+  };
+  for (uint32_t q = t; q < nq; q += NB)
+    if (qflag[q] == 1u) atomicAdd(hist + bucket(q), 1u);
+  __syncthreads();
+  // exclusive prefix over the buckets: per wave of 64, then over the 16 waves
+  const uint32_t lane = t & 63, wv = t >> 6;
+  const uint32_t v = hist[t];
+  uint32_t incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+    if ((int)lane >= o) incl += u;
+  }
+  if (lane == 63) part[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t i = 0; i < wv; i++) base += part[i];
+  __syncthreads();
+  hist[t] = base + incl - v;  // the bucket's first position
+  if (t == NB - 1) *n_out = base + incl;
+  __syncthreads();
+  for (uint32_t q = t; q < nq; q += NB)
+    if (qflag[q] == 1u) order[atomicAdd(hist + bucket(q), 1u)] = q;
+}
+
+hipError_t launch_schedule(const uint32_t* qflag, const float* prio, uint32_t nq, uint32_t* order, uint32_t* n_out,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(ngt_schedule_kernel, dim3(1), dim3(1024), 0, s, qflag, prio, nq, order, n_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_graph_search(const SearchArgs& a, int metric, int otype, uint32_t slots,
