@@ -792,6 +792,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     HIP_OK(hipMemsetAsync(c->qflag.p, 0, (size_t)nq * sizeof(uint32_t), s));
     SearchArgs p = a;
     p.pause_after = budget;
+    p.sched_prio = getenv("NGT_AMD_SCHED_PRIO") ? (uint32_t)std::max(0, std::min(2, atoi(getenv("NGT_AMD_SCHED_PRIO")))) : 0u;
     p.qstate = c->qstate.p;
     p.qstate_stride = lay.total;
     p.qflag = c->qflag.p;

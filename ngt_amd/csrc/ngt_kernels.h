@@ -112,6 +112,8 @@ struct SearchArgs {
   uint32_t* qflag;
   float* prio;
   unsigned long long* stat;      // [2]: expansions and queries finished by this launch (device sums) or null
+  uint32_t sched_prio;           // the probe's prediction: 0 unchecked keys within the exploration radius,
+                                 // 1 their margins sum (1 - d / radius_e), 2 keys within the result radius
 };
 
 // One paused query's saved state (the one-expansion kernel's accepted-only

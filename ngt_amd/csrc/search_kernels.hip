@@ -149,27 +149,35 @@ __device__ __forceinline__ void cq_chunk_min(const uint64_t* cq, uint64_t* cmin,
 // state to and from its record (PauseLayout).
 __device__ __forceinline__ void pause_save(uint8_t* prec, const PauseLayout& play, const SearchState& st,
                                           const uint64_t* spill, uint32_t ncq, uint32_t nspill, uint32_t nres,
-                                          float expr, float* prio, uint32_t* qflag) {
+                                          float expr, float radius, uint32_t mode, float* prio,
+                                          uint32_t* qflag) {
   const int lane = lane_id();
   uint64_t* rres = reinterpret_cast<uint64_t*>(prec + play.off_res);
   uint64_t* rcq = reinterpret_cast<uint64_t*>(prec + play.off_cq);
   uint64_t* rsp = reinterpret_cast<uint64_t*>(prec + play.off_spill);
   for (uint32_t i = lane; i < nres; i += 64) rres[i] = st.res[i];
-  uint32_t live = 0;
+  float live = 0.f;
+  auto score = [&](float d) -> float {
+    if (mode == 1) return d <= expr ? 1.0f - d / expr : 0.f;
+    if (mode == 2) return d <= radius ? 1.f : 0.f;
+    return d <= expr ? 1.f : 0.f;
+  };
   for (uint32_t i = lane; i < ncq; i += 64) {
     const uint64_t key = st.cq[i];
     rcq[i] = key;
-    live += key_dist(key) <= expr ? 1u : 0u;
+    live += score(key_dist(key));
   }
   for (uint32_t i = lane; i < nspill; i += 64) {
     const uint64_t key = spill[i];
     rsp[i] = key;
-    live += key_dist(key) <= expr ? 1u : 0u;
+    live += score(key_dist(key));
   }
-  // the predicted rest of the search: unchecked keys within the exploration radius
-  live = wave_sum_u32(live);
+  // the predicted rest of the search (default: unchecked keys within the
+  // exploration radius)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) live += __shfl_xor(live, o, 64);
   if (lane == 0) {
-    *prio = (float)live;
+    *prio = mode == 1 ? live * 16.f : live;
     *qflag = 1u;
   }
 }
@@ -671,7 +679,8 @@ __global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) 
         h->nedge = nedge;
         h->nexact = nexact;
       }
-      pause_save(prec, PauseLayout(a.k, a.cq_cap, 0), st, spill, ncq, nspill, nres, expr, a.prio + qi,
+      pause_save(prec, PauseLayout(a.k, a.cq_cap, 0), st, spill, ncq, nspill, nres, expr, radius, a.sched_prio,
+                 a.prio + qi,
                  a.qflag + qi);
       __syncthreads();
       continue;
