@@ -614,6 +614,10 @@ def main():
         else:
             log("phase cycles/query: pop %.3g adjacency+visited %.3g filter %.3g eval %.3g accept+rest %.3g "
                 "(sum %.3g)" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum()))
+    if "lacount" in os.environ.get("NGT_AMD_LIB", "") and ix.last_search_lookahead() >= 0:
+        m = c.mean(0)
+        log("lookahead line accounting/query: list entries %.0f, epoch probes %.0f, exact rows %.0f, spill keys "
+            "written %.0f read %.0f, refills %.0f; expansions %.0f" % (m[7], m[6], m[4], m[1], m[3], m[5], m[2]))
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "qg":
         tot = c[:, [4, 5, 6, 7]].mean(0)
         log("phase cycles/query: pop %.3g ids %.3g codes+adc %.3g accept %.3g (sum %.3g)" % (
@@ -1387,37 +1391,6 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
         print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
-
-
-def anng_child_line(args):
-    """The index a `ngt create` user has, measured beside the headline: the
-    1M ANNG (E 10) built on the device through the C API (files identical to
-    the reference's build), searched at the prf's EdgeSizeForSearch 40
-    (Command.cpp:39, Graph.h:675-692) from DVP-tree seeds.  A child process
-    of this bench (`--graph anng`), so its line carries its own roofline,
-    cpu_baseline, parity sample and reference checks; None if it fails."""
-    import subprocess
-    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--graph", "anng", "--anng-line", "off",
-           "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1", "--cpu-seconds", str(min(args.cpu_seconds, 8.0)),
-           "--latency-queries", "20"]
-    if args.no_cpu:
-        cmd.append("--no-cpu")
-    t0 = time.time()
-    log("ANNG line: %s" % " ".join(cmd[2:]))
-    env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
-        env.pop(k, None)
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=env, timeout=900)
-    out = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
-    if r.returncode != 0 or not out:
-        log("ANNG line failed (rc %d)" % r.returncode)
-        return {"error": "child run failed", "rc": r.returncode}
-    d = json.loads(out[-1])
-    d.pop("sweep", None)
-    d["child_wall_s"] = time.time() - t0
-    log("ANNG line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
-        d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
-    return d
 
 
 def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):

@@ -188,6 +188,11 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     // diagnostic build only: shader-clock totals per phase (wave 0's view)
     uint64_t t_a = 0, t_b = 0, t_c = 0, t_e = 0, t_f = 0, t_last = 0, nsteps = 0;
     (void)t_a; (void)t_b; (void)t_c; (void)t_e; (void)t_f; (void)t_last; (void)nsteps;
+    // diagnostic build only (NGT_AMD_LACOUNT): where a query's lines come from
+    // -- spill keys written / read, refills, visited-epoch probes, code rows of
+    // every list entry read (committed or not), exact rows
+    uint64_t n_spw = 0, n_spr = 0, n_refill = 0, n_probe = 0, n_codes = 0, n_rows = 0;
+    (void)n_spw; (void)n_spr; (void)n_refill; (void)n_probe; (void)n_codes; (void)n_rows;
     float radius = a.radius;
     float expr = 0.f;
     double frq = 0.0;
@@ -206,6 +211,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       } else {
         if (lane == 0) spill[nspill] = key;
         nspill++;
+#ifdef NGT_AMD_LACOUNT
+        n_spw++;
+#endif
       }
     };
     // move the LDS keys >= t to the spill (t lowers T)
@@ -224,6 +232,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           spill[nspill + mbcnt(mm)] = key;
         }
         if (nspill + nm <= a.spill_cap) nspill += nm;
+#ifdef NGT_AMD_LACOUNT
+        n_spw += nm;
+#endif
         __builtin_amdgcn_wave_barrier();
         if (keep) cq[out + mbcnt(km)] = key;
         __builtin_amdgcn_wave_barrier();
@@ -267,6 +278,10 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     auto refill = [&]() {
       const uint32_t want = a.cq_cap / 2;
       uint32_t* hist = nid;  // 64 counters (free outside the accept staging)
+#ifdef NGT_AMD_LACOUNT
+      n_refill++;
+      n_spr += 2 * nspill;  // the range pass and the move pass
+#endif
       // key distances as ordered 32-bit values; the spill keys within the radius
       const uint32_t lim = ord_of(expr);
       uint32_t lo = 0xffffffffu, hi = 0;
@@ -290,6 +305,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         const uint64_t width = (span + 63) / 64;
         hist[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
+#ifdef NGT_AMD_LACOUNT
+        n_spr += nspill;
+#endif
         for (uint32_t i = lane; i < nspill; i += 64) {
           const uint32_t o = (uint32_t)(spill[i] >> 32);
           if (o >= lo && o <= hi) atomicAdd(hist + (uint32_t)(((uint64_t)o - lo) / width), 1u);
@@ -670,6 +688,10 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             const uint32_t S = fsq + quad_sum_u32(cc - 2u * qc);
             const uint32_t e = base + 16u * j + (uint32_t)rs;
             const uint32_t id = ids[j];
+#ifdef NGT_AMD_LACOUNT
+            n_codes += (uint64_t)__popcll(ballot64(g == 0 && e < nl));
+            n_probe += (uint64_t)__popcll(ballot64(g == 0 && e < nl && bit[j]));
+#endif
             if (g == 0 && e < nl) {
               const bool fresh = !bit[j] || ((pw[j] >> (8 * (id & 3))) & 0xffu) != epoch;
               lfl[e] = (uint8_t)((fresh ? 1u : 0u) | (fresh && S <= fthr ? 2u : 0u));
@@ -751,6 +773,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       }
       __syncthreads();
       NGT_MARK(t_e);
+#ifdef NGT_AMD_LACOUNT
+      n_rows += xtot;
+#endif
 
       // F. wave 0 commits in the reference's pop order.  After commits
       // 0..j-1 the unchecked set is the step-start set minus t_0..t_{j-1}
@@ -842,6 +867,17 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           c[5] = maxq;
           c[6] = nexact;  // exact neighbour distances of the committed expansions
           c[7] = ns;
+#ifdef NGT_AMD_LACOUNT
+          // line accounting: [1] spill keys written, [3] spill keys read,
+          // [5] refills, [6] epoch probes, [7] list entries' code rows;
+          // [4] exact rows (committed or not)
+          c[1] = n_spw;
+          c[3] = n_spr;
+          c[5] = n_refill;
+          c[6] = n_probe;
+          c[7] = n_codes;
+          c[4] = n_rows;
+#endif
 #ifdef NGT_AMD_STAMPS
           // phase cycles: [5] pop + targets, [6] adjacency + lists, [1] filter
           // + survivors, [7] exact rows, [3] commit; [4] steps
