@@ -546,6 +546,7 @@ def main():
     qps = NQ * (1 if shard else world) * args.steps / elapsed
 
     c = cnt.cpu().numpy().astype(np.float64)
+    c_timed = c
     evals_per_query = None
     if not qgm and args.visited == -2:
         # The timed runs keep only accepted ids in the visited set, so their
@@ -615,7 +616,7 @@ def main():
             log("phase cycles/query: pop %.3g adjacency+visited %.3g filter %.3g eval %.3g accept+rest %.3g "
                 "(sum %.3g)" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum()))
     if "lacount" in os.environ.get("NGT_AMD_LIB", "") and ix.last_search_lookahead() >= 0:
-        m = c.mean(0)
+        m = c_timed.mean(0)  # the timed launches' (visited set as timed) counters
         log("lookahead line accounting/query: list entries %.0f, epoch probes %.0f, exact rows %.0f, spill keys "
             "written %.0f read %.0f, refills %.0f; expansions %.0f" % (m[7], m[6], m[4], m[1], m[3], m[5], m[2]))
     if "stamps" in os.environ.get("NGT_AMD_LIB", "") and args.mode == "qg":

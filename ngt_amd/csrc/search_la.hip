@@ -660,11 +660,14 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             const uint32_t e = base + 16u * j + (uint32_t)rs;
             const uint32_t id = e < nl ? L[e] : 0u;
             ids[j] = id;
-            bit[j] = id != 0u && vf_test(vf, vf_shift, id);
             pw[j] = 0u;
-            if (bit[j] && g == 0)
-              pw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
+            bit[j] = false;
+            if constexpr (FULL) {
+              bit[j] = id != 0u && vf_test(vf, vf_shift, id);
+              if (bit[j] && g == 0)
+                pw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+            }
             const uint2* cp = reinterpret_cast<const uint2*>(a.fcodes + (uint64_t)id * (4 * E)) + g * NW;
             if (base + 16u * j < nl) {
 #pragma unroll
@@ -690,11 +693,18 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             const uint32_t id = ids[j];
 #ifdef NGT_AMD_LACOUNT
             n_codes += (uint64_t)__popcll(ballot64(g == 0 && e < nl));
-            n_probe += (uint64_t)__popcll(ballot64(g == 0 && e < nl && bit[j]));
+            if constexpr (FULL) n_probe += (uint64_t)__popcll(ballot64(g == 0 && e < nl && bit[j]));
 #endif
             if (g == 0 && e < nl) {
-              const bool fresh = !bit[j] || ((pw[j] >> (8 * (id & 3))) & 0xffu) != epoch;
-              lfl[e] = (uint8_t)((fresh ? 1u : 0u) | (fresh && S <= fthr ? 2u : 0u));
+              if constexpr (FULL) {
+                const bool fresh = !bit[j] || ((pw[j] >> (8 * (id & 3))) & 0xffu) != epoch;
+                lfl[e] = (uint8_t)((fresh ? 1u : 0u) | (fresh && S <= fthr ? 2u : 0u));
+              } else {
+                // accepted-only set: only a survivor can be accepted, so only
+                // survivors need the visited test -- it rides with their exact
+                // rows (phase E) instead of an epoch probe per list entry
+                lfl[e] = (uint8_t)(1u | (S <= fthr ? 2u : 0u));
+              }
             }
           }
         }
@@ -752,10 +762,22 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
         for (uint32_t r0 = (uint32_t)wave * 16u * EG; r0 < xtot; r0 += 16u * EG * W) {
           float4 v[EG][NCH];
+          uint32_t xid[EG], xpw[EG];
+          bool xchk[EG];
 #pragma unroll
           for (int j = 0; j < EG; j++) {
             const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
             const uint32_t id = rr < xtot ? X[rr] : 0u;
+            xid[j] = id;
+            xpw[j] = 0u;
+            xchk[j] = false;
+            if constexpr (!FULL) {
+              // the survivor's visited test: LDS filter, then its HBM epoch
+              xchk[j] = g == 0 && rr < xtot && vf_test(vf, vf_shift, id);
+              if (xchk[j])
+                xpw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
             const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)id * a.row_bytes) + g;
             if (j == 0 || r0 + 16u * j < xtot) {
 #pragma unroll
@@ -767,7 +789,13 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             if (j != 0 && r0 + 16u * j >= xtot) continue;
             const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
             const float d = l2_fold_rows<NCH>(qq, v[j]);
-            if (g == 0 && rr < xtot) Xd[rr] = d;
+            // accepted-only set: a visited survivor is marked by a negative
+            // distance (an L2 distance is never below +0)
+            const bool seen = xchk[j] && ((xpw[j] >> (8 * (xid[j] & 3))) & 0xffu) == epoch;
+            if (g == 0 && rr < xtot) Xd[rr] = seen ? -1.f : d;
+#ifdef NGT_AMD_LACOUNT
+            n_probe += (uint64_t)__popcll(ballot64(xchk[j]));
+#endif
           }
         }
       }
@@ -812,22 +840,33 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             const uint64_t kmask = ballot64((fl & 2u) != 0u);  // positions in X
             const uint32_t xi = xr + mbcnt(kmask);
             xr += (uint32_t)__popcll(kmask);
-            const bool fresh = (fl & 1u) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
-            const uint32_t nfresh = (uint32_t)__popcll(ballot64(fresh));
+            bool keep;
+            float xd = 0.f;
             if constexpr (FULL) {
+              const bool fresh = (fl & 1u) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
+              const uint32_t nfresh = (uint32_t)__popcll(ballot64(fresh));
               if (fresh) {
                 vf_set(vf, vf_shift, id);
                 vis[id] = (uint8_t)epoch;
                 sh_insert(sh, a.la_sh_log2, id);
               }
               sh_used += nfresh;
+              ndist += nfresh;
+              keep = fresh && (fl & 2u);
+              if (keep) xd = Xd[xi];
+            } else {
+              // survivors carry their visited test (negative distance =
+              // accepted before this step; the step's id set = accepted by
+              // its earlier commits); every other entry counts as evaluated
+              const bool surv = (fl & 2u) != 0u;
+              if (surv) xd = Xd[xi];
+              keep = surv && !(xd < 0.f) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
+              ndist += (uint32_t)__popcll(ballot64(in && (!surv || keep)));
             }
-            ndist += nfresh;
-            const bool keep = fresh && (fl & 2u);
             const uint64_t km = ballot64(keep);
             if (keep) {
               nid[mbcnt(km)] = id;
-              nd[mbcnt(km)] = Xd[xi];
+              nd[mbcnt(km)] = xd;
             }
             __builtin_amdgcn_wave_barrier();
             const uint32_t me = (uint32_t)__popcll(km);
