@@ -251,7 +251,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-launches", type=int, default=0,
                     help="after the epsilon is set: run this many launches of the timed configuration and exit")
-    ap.add_argument("--streams", type=int, default=2, help="HIP streams consecutive steps alternate over")
+    ap.add_argument("--streams", type=int, default=3, help="HIP streams consecutive steps alternate over")
     ap.add_argument("--anng-line", choices=["auto", "on", "off"], default="auto",
                     help="attach the NGT-built index's line (a child run of --graph anng) as the 'anng' key; "
                          "auto = on for the default single-GPU C2 run")
