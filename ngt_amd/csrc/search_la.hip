@@ -48,7 +48,7 @@ struct LaCtl {
 // 16-byte aligned LDS carve-out; the host's search_la_lds_bytes mirrors it.
 struct LaLayout {
   uint32_t off_tkey, off_tcnt, off_loff, off_xoff, off_vf, off_cq, off_res, off_q, off_qb, off_l,
-      off_lfl, off_x, off_xd, off_sh, off_nid, off_nd, total;
+      off_lfl, off_x, off_xe, off_xd, off_sh, off_nid, off_nd, total;
   __host__ __device__ static uint32_t up16(uint32_t v) { return (v + 15u) & ~15u; }
   __host__ __device__ LaLayout(const SearchArgs& a, int P) {
     uint32_t o = up16(sizeof(LaCtl));
@@ -64,6 +64,7 @@ struct LaLayout {
     off_l = o; o = up16(o + 4u * a.la_lmax);
     off_lfl = o; o = up16(o + a.la_lmax);
     off_x = o; o = up16(o + 4u * a.la_lmax);
+    off_xe = o; o = up16(o + 4u * a.la_lmax);
     off_xd = o; o = up16(o + 4u * a.la_lmax);
     off_sh = o; o = up16(o + (4u << a.la_sh_log2));
     off_nid = o; o = up16(o + 256u);
@@ -129,7 +130,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
   uint32_t* L = reinterpret_cast<uint32_t*>(smem + lay.off_l);
   uint8_t* lfl = smem + lay.off_lfl;
   uint32_t* X = reinterpret_cast<uint32_t*>(smem + lay.off_x);
-  float* Xd = reinterpret_cast<float*>(smem + lay.off_xd);
+  uint32_t* Xe = reinterpret_cast<uint32_t*>(smem + lay.off_xe);
+  float* Xd = reinterpret_cast<float*>(smem + lay.off_xd);  // by list entry
   uint32_t* sh = reinterpret_cast<uint32_t*>(smem + lay.off_sh);
   uint32_t* nid = reinterpret_cast<uint32_t*>(smem + lay.off_nid);
   float* nd = reinterpret_cast<float*>(smem + lay.off_nd);
@@ -610,20 +612,38 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       }
       // the step hash starts empty
       for (uint32_t i = tid; i < sh_n; i += NT) sh[i] = 0u;
-      __syncthreads();
+      if constexpr (W > 1) __syncthreads();
       // list offsets: the targets whose lists fit the list capacity (t0 always does)
       uint32_t ntl = nt, tot = 0;
       uint32_t myoff[PW];
 #pragma unroll
       for (int jj = 0; jj < PW; jj++) myoff[jj] = 0xffffffffu;
-      for (uint32_t j = 0; j < nt; j++) {
-        const uint32_t c = tcnt[j];
-        if (tot + c > lmax) { ntl = j; break; }
+      if constexpr (W == 1) {
+        // every target's count is in this wave's registers
+        bool fits = true;
 #pragma unroll
-        for (int jj = 0; jj < PW; jj++)
-          if (j == (uint32_t)(wave + W * jj)) myoff[jj] = tot;
-        if (tid == 0) loff[j] = tot;
-        tot += c;
+        for (int jj = 0; jj < PW; jj++) {
+          if ((uint32_t)jj < nt && fits) {
+            if (tot + cnt[jj] > lmax) {
+              ntl = (uint32_t)jj;
+              fits = false;
+            } else {
+              myoff[jj] = tot;
+              if (tid == 0) loff[jj] = tot;
+              tot += cnt[jj];
+            }
+          }
+        }
+      } else {
+        for (uint32_t j = 0; j < nt; j++) {
+          const uint32_t c = tcnt[j];
+          if (tot + c > lmax) { ntl = j; break; }
+#pragma unroll
+          for (int jj = 0; jj < PW; jj++)
+            if (j == (uint32_t)(wave + W * jj)) myoff[jj] = tot;
+          if (tid == 0) loff[j] = tot;
+          tot += c;
+        }
       }
       if (tid == 0) {
         loff[ntl] = tot;
@@ -647,6 +667,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       // quad per entry, RG groups of 16 entries in flight per wave
       {
         const uint32_t fthr = ctl->fthr, fsq = ctl->fsq;
+        uint32_t xrun = 0;  // W == 1: survivors so far, entry order
         uint2 q[NW];
         const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
 #pragma unroll
@@ -695,24 +716,36 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             n_codes += (uint64_t)__popcll(ballot64(g == 0 && e < nl));
             if constexpr (FULL) n_probe += (uint64_t)__popcll(ballot64(g == 0 && e < nl && bit[j]));
 #endif
-            if (g == 0 && e < nl) {
-              if constexpr (FULL) {
-                const bool fresh = !bit[j] || ((pw[j] >> (8 * (id & 3))) & 0xffu) != epoch;
-                lfl[e] = (uint8_t)((fresh ? 1u : 0u) | (fresh && S <= fthr ? 2u : 0u));
-              } else {
-                // accepted-only set: only a survivor can be accepted, so only
-                // survivors need the visited test -- it rides with their exact
-                // rows (phase E) instead of an epoch probe per list entry
-                lfl[e] = (uint8_t)(1u | (S <= fthr ? 2u : 0u));
+            bool fresh = true;
+            if constexpr (FULL) fresh = !bit[j] || ((pw[j] >> (8 * (id & 3))) & 0xffu) != epoch;
+            // accepted-only set: only a survivor can be accepted, so only
+            // survivors need the visited test -- it rides with their exact
+            // rows (phase E) instead of an epoch probe per list entry
+            const bool sv = g == 0 && e < nl && fresh && S <= fthr;
+            if (g == 0 && e < nl) lfl[e] = (uint8_t)((fresh ? 1u : 0u) | (sv ? 2u : 0u));
+            if constexpr (W == 1) {
+              const uint64_t sm = ballot64(sv);
+              if (sv) {
+                X[xrun + mbcnt(sm)] = id;
+                Xe[xrun + mbcnt(sm)] = e;
               }
+              xrun += (uint32_t)__popcll(sm);
             }
           }
+        }
+        if constexpr (W == 1) {
+          if (lane == 0) ctl->nx = xrun;
         }
       }
       __syncthreads();
 
-      // D. survivors (keep bits) of every target, in target then neighbour order
+      // D. survivors (keep bits) of every target, in target then neighbour
+      // order (one wave: collected in phase C already)
       const uint32_t ntl_s = ctl->ntl;
+      uint32_t xtot = 0;
+      if constexpr (W == 1) {
+        xtot = ctl->nx;
+      } else {
       uint32_t xc[PW];
 #pragma unroll
       for (int jj = 0; jj < PW; jj++) {
@@ -727,7 +760,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if (lane == 0) xoff[j] = xc[jj];  // count; prefix below
       }
       __syncthreads();
-      uint32_t xo[PW], xtot = 0;
+      uint32_t xo[PW];
 #pragma unroll
       for (int jj = 0; jj < PW; jj++) xo[jj] = 0;
       for (uint32_t j = 0; j < ntl_s; j++) {
@@ -749,11 +782,15 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           const uint32_t e = e0 + (uint32_t)lane;
           const bool kp = e < le && (lfl[e] & 2u);
           const uint64_t km = ballot64(kp);
-          if (kp) X[o + mbcnt(km)] = L[e];
+          if (kp) {
+            X[o + mbcnt(km)] = L[e];
+            Xe[o + mbcnt(km)] = e;
+          }
           o += (uint32_t)__popcll(km);
         }
       }
       __syncthreads();
+      }
 
       NGT_MARK(t_c);
       // E. exact comparator distances of the survivors (bit-identical to
@@ -792,7 +829,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             // accepted-only set: a visited survivor is marked by a negative
             // distance (an L2 distance is never below +0)
             const bool seen = xchk[j] && ((xpw[j] >> (8 * (xid[j] & 3))) & 0xffu) == epoch;
-            if (g == 0 && rr < xtot) Xd[rr] = seen ? -1.f : d;
+            if (g == 0 && rr < xtot) Xd[Xe[rr]] = seen ? -1.f : d;
 #ifdef NGT_AMD_LACOUNT
             n_probe += (uint64_t)__popcll(ballot64(xchk[j]));
 #endif
@@ -831,15 +868,11 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           nexp++;
           const uint32_t lb = loff[j], le = loff[j + 1];
           nedge += le - lb;
-          uint32_t xr = xoff[j];
           for (uint32_t e0 = lb; e0 < le; e0 += 64) {
             const uint32_t e = e0 + (uint32_t)lane;
             const bool in = e < le;
             const uint32_t id = in ? L[e] : 0u;
             const uint32_t fl = in ? lfl[e] : 0u;
-            const uint64_t kmask = ballot64((fl & 2u) != 0u);  // positions in X
-            const uint32_t xi = xr + mbcnt(kmask);
-            xr += (uint32_t)__popcll(kmask);
             bool keep;
             float xd = 0.f;
             if constexpr (FULL) {
@@ -853,13 +886,13 @@ ngt_graph_search_la_kernel(SearchArgs a) {
               sh_used += nfresh;
               ndist += nfresh;
               keep = fresh && (fl & 2u);
-              if (keep) xd = Xd[xi];
+              if (keep) xd = Xd[e];
             } else {
               // survivors carry their visited test (negative distance =
               // accepted before this step; the step's id set = accepted by
               // its earlier commits); every other entry counts as evaluated
               const bool surv = (fl & 2u) != 0u;
-              if (surv) xd = Xd[xi];
+              if (surv) xd = Xd[e];
               keep = surv && !(xd < 0.f) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
               ndist += (uint32_t)__popcll(ballot64(in && (!surv || keep)));
             }
