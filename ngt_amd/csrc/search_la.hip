@@ -43,6 +43,9 @@ namespace ngt_amd {
 struct LaCtl {
   uint32_t qi, done, nt, ntl, nl, nx, fthr, fsq;
   uint32_t epoch, pad[7];
+  // the filter threshold's double-precision terms, kept in LDS: in registers
+  // they spill, and a scratch reload waits for every store still in flight
+  double fe, finv_b, frq;
 };
 
 // 16-byte aligned LDS carve-out; the host's search_la_lds_bytes mirrors it.
@@ -144,8 +147,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
   const uint32_t vf_shift = 32 - a.vf_log2;
   const uint32_t sh_n = 1u << a.la_sh_log2;
   const uint32_t lmax = a.la_lmax;
-  const float fa = a.fparams[0], fb = a.fparams[1], fe = a.fparams[2];
-  const double finv_b = 1.0 / (double)fb;
+  const float fa = a.fparams[0], fb = a.fparams[1];
   const uint32_t slot = blockIdx.x;
   uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
   uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
@@ -186,7 +188,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     uint64_t tk[P];
 #pragma unroll
     for (int j = 0; j < P; j++) tk[j] = ~0ull;
-    uint32_t nt0 = 0, nblock = P, cur_j = 0;
+    uint32_t nblock = P, cur_j = 0;
     // diagnostic build only: shader-clock totals per phase (wave 0's view)
     uint64_t t_a = 0, t_b = 0, t_c = 0, t_e = 0, t_f = 0, t_last = 0, nsteps = 0;
     (void)t_a; (void)t_b; (void)t_c; (void)t_e; (void)t_f; (void)t_last; (void)nsteps;
@@ -198,14 +200,19 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     float radius = a.radius;
     float expr = 0.f;
     double frq = 0.0;
-    // ---- the unchecked set: two levels with a key threshold T ------------
-    // LDS keys are all < T <= every spill key (HBM, per slot), so the
-    // smallest keys are always in LDS while LDS is non-empty (no spill
-    // scan).  A full LDS is compacted (keys beyond the exploration radius can
-    // never be popped, Graph.cpp:433-435) and, if still over half full, its
-    // larger half moves to the spill (T drops); an empty LDS refills with
-    // the smallest spill keys (T rises).  Exact throughout.  The LDS keys are
-    // unsorted: a step's targets come from one scan of them (phase A).
+    // ---- the unchecked set: three levels with key thresholds B and T -------
+    // head (wave 0's registers, sorted: lane i = i-th smallest, hn keys) < B
+    // <= tail (LDS, unsorted, ncq keys) < T <= spill (HBM, per slot), so the
+    // smallest keys are always in the head while it is non-empty: a step's
+    // targets are its first lanes and a pop is a lane shift.  A full head
+    // sends its largest key to the tail (B drops); an emptying head takes the
+    // smallest tail keys (histogram threshold + bitonic sort, B rises).  A full
+    // tail is compacted (keys beyond the exploration radius can never be
+    // popped, Graph.cpp:433-435) and, if still over half full, its larger half
+    // moves to the spill (T drops); an empty tail refills with the smallest
+    // spill keys (T rises).  Exact throughout.
+    uint64_t hk = ~0ull, B = ~0ull;
+    uint32_t hn = 0;
     uint64_t T = ~0ull;
     auto spill_push = [&](uint64_t key) {
       if (nspill >= a.spill_cap) {
@@ -356,7 +363,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       T = nspill ? ((uint64_t)bound << 32) : ~0ull;
       __builtin_amdgcn_wave_barrier();
     };
-    auto insert_key = [&](uint64_t key) {
+    auto tail_insert = [&](uint64_t key) {
       if (key >= T) {
         spill_push(key);
       } else {
@@ -368,8 +375,85 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           ncq++;
         }
       }
-      if (ncq + nspill > maxq) maxq = ncq + nspill;
       __builtin_amdgcn_wave_barrier();
+    };
+    auto insert_key = [&](uint64_t key) {
+      if (key < B) {
+        const uint32_t pos = (uint32_t)__popcll(ballot64((uint32_t)lane < hn && hk < key));
+        const uint64_t uk = wave_up1_u64(hk);
+        if (hn == 64u) {
+          // the head is full: its largest key (or this one) moves to the tail
+          if (pos == 64u) {
+            B = key;
+            tail_insert(key);
+          } else {
+            const uint64_t e = readlane_u64(hk, 63);
+            if ((uint32_t)lane > pos) hk = uk;
+            if ((uint32_t)lane == pos) hk = key;
+            B = e;
+            tail_insert(e);
+          }
+        } else {
+          if ((uint32_t)lane > pos && (uint32_t)lane <= hn) hk = uk;
+          if ((uint32_t)lane == pos) hk = key;
+          hn++;
+        }
+      } else {
+        tail_insert(key);
+      }
+      if (hn + ncq + nspill > maxq) maxq = hn + ncq + nspill;
+    };
+    // fill the head up with the smallest tail keys (the tail takes the
+    // smallest spill keys first when it is empty): at most 64 - hn keys, all
+    // above the head's, move in; then a bitonic sort across the lanes
+    auto refill_head = [&]() {
+      if (ncq == 0 && nspill != 0) refill();
+      if (ncq == 0) return;
+      const uint32_t room = 64u - hn;
+      const uint64_t t = lat_select(cq, ncq, room, ~0ull, nid);
+      uint64_t* st64 = reinterpret_cast<uint64_t*>(nid);  // 64 x u64 staged through nid/nd (adjacent)
+      uint32_t got = 0, out = 0;
+      for (uint32_t b0 = 0; b0 < ncq; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < ncq ? cq[i] : ~0ull;
+        const bool mv = i < ncq && key < t;
+        const bool kp = i < ncq && !mv;
+        const uint64_t mm = ballot64(mv), km = ballot64(kp);
+        __builtin_amdgcn_wave_barrier();
+        if (mv && got + mbcnt(mm) < room) st64[got + mbcnt(mm)] = key;
+        if (kp) cq[out + mbcnt(km)] = key;
+        __builtin_amdgcn_wave_barrier();
+        got += (uint32_t)__popcll(mm);
+        out += (uint32_t)__popcll(km);
+      }
+      if (got == 0u || got > room) {
+        if (lane == 0) atomicOr(a.error, 8);  // selection check: never expected
+        got = got > room ? room : got;
+      }
+      ncq = out;
+      uint64_t v = (uint32_t)lane < hn ? hk : ((uint32_t)lane < hn + got ? st64[lane - hn] : ~0ull);
+      __builtin_amdgcn_wave_barrier();
+      // bitonic sort of the 64 lanes (ascending; empty lanes hold ~0)
+#pragma unroll
+      for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+          const uint64_t o = shfl_xor_u64(v, j);
+          const bool up = ((lane & kk) == 0);
+          const bool lower = (lane & j) == 0;
+          const uint64_t mn = o < v ? o : v, mx = o < v ? v : o;
+          v = (lower == up) ? mn : mx;
+        }
+      }
+      hk = v;
+      hn += got;
+      B = (ncq + nspill) ? readlane_u64(hk, (int)hn - 1) + 1 : ~0ull;
+    };
+    // the head's first key leaves (the commit of a target)
+    auto pop_head = [&]() {
+      const uint64_t dk = wave_down1_u64(hk);
+      hk = (uint32_t)lane + 1 < hn ? dk : ~0ull;
+      hn--;
     };
     // keys entering the unchecked set during the commit of target cur_j: the
     // first later target they precede can no longer be the reference's next
@@ -409,19 +493,33 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         sh_used += cnt;
       }
       note_pushed(mine, key);
-      const bool below = ballot64(mine && key >= T) == 0ull;
-      if (below && ncq + cnt <= a.cq_cap) {
-        if (mine) cq[ncq + mbcnt(bm)] = key;
-        ncq += cnt;
-        __builtin_amdgcn_wave_barrier();
-        if (ncq + nspill > maxq) maxq = ncq + nspill;
-      } else {
-        uint64_t r = bm;
-        while (r) {
-          const int j = __ffsll((long long)r) - 1;
-          r &= r - 1;
-          insert_key(__shfl(key, j, 64));
+      // keys below B enter the head one at a time (sorted insert); the rest
+      // go to the tail, in one append when they all lie below T and fit
+      const uint64_t hm = ballot64(mine && key < B);
+      const uint64_t tm = bm & ~hm;
+      uint64_t r = hm;
+      while (r) {
+        const int j = __ffsll((long long)r) - 1;
+        r &= r - 1;
+        insert_key(__shfl(key, j, 64));
+      }
+      const uint32_t tc = (uint32_t)__popcll(tm);
+      if (tc) {
+        const bool tmine = (tm >> lane) & 1ull;
+        const bool below = ballot64(tmine && key >= T) == 0ull;
+        if (below && ncq + tc <= a.cq_cap) {
+          if (tmine) cq[ncq + mbcnt(tm)] = key;
+          ncq += tc;
+          __builtin_amdgcn_wave_barrier();
+        } else {
+          r = tm;
+          while (r) {
+            const int j = __ffsll((long long)r) - 1;
+            r &= r - 1;
+            tail_insert(__shfl(key, j, 64));
+          }
         }
+        if (hn + ncq + nspill > maxq) maxq = hn + ncq + nspill;
       }
     };
     // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
@@ -470,6 +568,11 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     if (wave == 0) {
       uint32_t fsq = 0;
       filter_query(qlds, a.dp, fa, fb, qb, fsq, frq);
+      if (lane == 0) {
+        ctl->fe = (double)a.fparams[2];
+        ctl->finv_b = 1.0 / (double)a.fparams[1];
+        ctl->frq = frq;
+      }
       if (lane == 0) ctl->fsq = fsq;
       // ---- setupDistances + setupSeeds (Graph.cpp:293-367) --------------
       const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
@@ -507,72 +610,16 @@ ngt_graph_search_la_kernel(SearchArgs a) {
 #endif
     for (;;) {
       // A. wave 0: the reference's next pop and the keys in line after it --
-      // the nt <= P smallest keys of the unchecked set within the exploration
-      // radius (all in LDS: spill keys are >= T > every LDS key).  Every lane
-      // keeps the two smallest keys of its share (with positions), the wave
-      // takes the minimum of the lanes' heads nt times, and a lane that runs
-      // out of heads rescans its share above the last key it gave.  The
-      // targets leave the LDS array now; those the commit does not reach go
-      // back at the end of the step.
+      // the nt <= P smallest keys of the unchecked set within the
+      // exploration radius: the head's first lanes (refilled from the tail
+      // when it holds fewer than P keys).  They stay in the head; each
+      // committed target leaves it at its commit (phase F).
       if (wave == 0) {
-        if (ncq == 0 && nspill != 0) refill();
-        uint32_t nt = 0;
-        uint32_t tix[P];
-        {
-          uint64_t h0 = ~0ull, h1 = ~0ull;
-          uint32_t i0 = 0, i1 = 0;
-          for (uint32_t i = lane; i < ncq; i += 64) {
-            const uint64_t v = cq[i];
-            if (v < h1) {
-              if (v < h0) { h1 = h0; i1 = i0; h0 = v; i0 = i; } else { h1 = v; i1 = i; }
-            }
-          }
+        if (hn < (uint32_t)P && (ncq | nspill) != 0u) refill_head();
+        const uint32_t lim = hn < (uint32_t)P ? hn : (uint32_t)P;
+        const uint32_t nt = (uint32_t)__popcll(ballot64((uint32_t)lane < lim && key_dist(hk) <= expr));
 #pragma unroll
-          for (int j = 0; j < P; j++) {
-            tk[j] = ~0ull;
-            tix[j] = 0u;
-            if ((uint32_t)j != nt) continue;  // an earlier key ended the list
-            const uint64_t m = uniform_u64(wave_min_u64(h0));
-            if (m == ~0ull || key_dist(m) > expr) continue;
-            const int ol = __ffsll((long long)ballot64(h0 == m)) - 1;  // keys are distinct: one owner
-            tk[j] = m;
-            tix[j] = (uint32_t)__builtin_amdgcn_readlane((int)i0, ol);
-            nt++;
-            if (j + 1 < P && lane == ol) {
-              h0 = h1;
-              i0 = i1;
-              h1 = ~0ull;
-              if (h0 == ~0ull) {
-                for (uint32_t i = lane; i < ncq; i += 64) {
-                  const uint64_t v = cq[i];
-                  if (v > m && v < h1) {
-                    if (v < h0) { h1 = h0; i1 = i0; h0 = v; i0 = i; } else { h1 = v; i1 = i; }
-                  }
-                }
-              }
-            }
-          }
-        }
-        // swap-remove the targets, highest position first (a moved tail key
-        // is never a target still to remove)
-#pragma unroll
-        for (int x = 0; x < P; x++)
-#pragma unroll
-          for (int y = x + 1; y < P; y++)
-            if (tix[y] > tix[x] && (uint32_t)y < nt) {
-              const uint32_t t = tix[x];
-              tix[x] = tix[y];
-              tix[y] = t;
-            }
-#pragma unroll
-        for (int x = 0; x < P; x++) {
-          if ((uint32_t)x < nt) {
-            if (lane == 0) cq[tix[x]] = cq[ncq - 1];
-            __builtin_amdgcn_wave_barrier();
-            ncq--;
-          }
-        }
-        nt0 = nt;
+        for (int j = 0; j < P; j++) tk[j] = (uint32_t)j < nt ? readlane_u64(hk, j) : ~0ull;
         const uint32_t done = nt == 0 ? 1u : 0u;  // empty, or the minimum is beyond the radius (Graph.cpp:433-435)
         if (lane == 0) {
 #pragma unroll
@@ -582,7 +629,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if (lane == 0) {
           ctl->done = done;
           ctl->nt = nt;
-          ctl->fthr = filter_threshold(expr, (double)fe, finv_b, frq);
+          ctl->fthr = filter_threshold(expr, ctl->fe, ctl->finv_b, ctl->frq);
         }
       }
       __syncthreads();
@@ -864,6 +911,10 @@ ngt_graph_search_la_kernel(SearchArgs a) {
               break;
             }
           }
+          // t_j is the head's first key here: t_0..t_{j-1} left it and no
+          // key pushed since precedes t_j (nblock > j)
+          if (readlane_u64(hk, 0) != tk_at(j) && lane == 0) atomicOr(a.error, 8);
+          pop_head();
           ncommit++;
           nexp++;
           const uint32_t lb = loff[j], le = loff[j + 1];
@@ -909,12 +960,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           }
         }
         ndisc += ntl_s - ncommit;
-        if (done) {
-          if (lane == 0) ctl->done = 1;
-        } else {
-          // the targets the commit did not reach return to the unchecked set
-          for (uint32_t j = ncommit; j < nt0; j++) insert_key(tk_at(j));
-        }
+        // the targets the commit did not reach are still in the head
+        if (done && lane == 0) ctl->done = 1;
       }
       __syncthreads();
       NGT_MARK(t_f);

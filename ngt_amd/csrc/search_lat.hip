@@ -85,37 +85,6 @@ struct LatLayout {
   }
 };
 
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-// whole-wave lane shifts by one on the DPP path (gfx9 wave_shr:1 /
-// wave_shl:1: one VALU op instead of an LDS-crossbar ds_bpermute): up1 gives
-// lane i the value of lane i-1, down1 the value of lane i+1; the lane with
-// no source keeps its own value (the callers overwrite or mask it)
-__device__ __forceinline__ uint32_t wave_up1(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint32_t wave_down1(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint64_t wave_up1_u64(uint64_t v) {
-  return ((uint64_t)wave_up1((uint32_t)(v >> 32)) << 32) | wave_up1((uint32_t)v);
-}
-__device__ __forceinline__ uint64_t wave_down1_u64(uint64_t v) {
-  return ((uint64_t)wave_down1((uint32_t)(v >> 32)) << 32) | wave_down1((uint32_t)v);
-}
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t uniform_u64_lat(uint64_t v) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
 __device__ __forceinline__ bool bm_test(const uint32_t* bm, uint32_t id) { return (bm[id >> 5] >> (id & 31)) & 1u; }
 
 __device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
@@ -123,57 +92,6 @@ __device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
 }
 __device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// A threshold t over the keys of arr[0..n) that are <= lim (wave-uniform
-// arguments): at most M keys lie below t, at least one does, and M/2 or more
-// when the keys allow.  Histogram passes over 64 power-of-two bins of the key
-// range (64 LDS counters in hist), refining the first bin that overflows.
-// Returns 0 when no key is <= lim.  Not inlined: it runs a few times per
-// query and would otherwise share the commit loop's registers.
-__device__ __noinline__ uint64_t lat_select(const uint64_t* arr, uint32_t n, uint32_t M, uint64_t lim, uint32_t* hist) {
-  const int lane = lane_id();
-  uint64_t lo = ~0ull, hi = 0;
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint64_t v = arr[i];
-    if (v <= lim) {
-      lo = v < lo ? v : lo;
-      hi = v > hi ? v : hi;
-    }
-  }
-  lo = uniform_u64_lat(wave_min_u64(lo));
-  hi = uniform_u64_lat(~wave_min_u64(~hi));
-  if (lo > hi) return 0ull;
-  uint32_t base = 0;
-  for (int it = 0; it < 16; it++) {
-    const uint64_t span = hi - lo;
-    const int bits = span ? 64 - __clzll((long long)span) : 0;
-    const int shift = bits > 6 ? bits - 6 : 0;
-    // hist is LDS reached through a generic pointer: flat accesses may
-    // complete out of order, so each phase drains before the next
-    hist[lane] = 0u;
-    __threadfence_block();
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint64_t v = arr[i];
-      if (v >= lo && v <= hi && v <= lim) atomicAdd(hist + (uint32_t)((v - lo) >> shift), 1u);
-    }
-    __threadfence_block();
-    uint32_t incl = hist[lane];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
-      if (lane >= o) incl += u;
-    }
-    const uint32_t b = (uint32_t)__popcll(ballot64(base + incl <= M));  // bins [0, b) fit
-    if (b == 64u) return hi + 1;
-    const uint32_t below = base + (b ? (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)b - 1) : 0u);
-    if ((below >= M / 2 && below > 0) || shift == 0) return lo + ((uint64_t)b << shift);
-    base = below;
-    lo = lo + ((uint64_t)b << shift);
-    const uint64_t top = lo + ((1ull << shift) - 1ull);
-    hi = top < hi ? top : hi;
-  }
-  return lo + 1;  // never expected: the minimum alone
 }
 
 // ---- serving form (ngt_kernels.h ServeArgs) ---------------------------------
