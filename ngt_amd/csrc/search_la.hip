@@ -471,19 +471,16 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if ((uint32_t)jj == j) r = tk[jj];
       return r;
     };
-    // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
-    // order (Graph.cpp:471-483); only candidates within the radius at batch
-    // start can be accepted
-    // Push the candidates of `bm` (lanes of nid/nd, all within the
+    // Push the candidates of `bm` (lanes of cid/cd, all within the
     // exploration radius and none within the result radius, so none changes
     // either radius) into the unchecked set at once -- what the sequential
     // accept would do for each of them.
-    auto push_batch = [&](uint64_t bm) {
+    auto push_batch = [&](uint64_t bm, uint32_t cid, float cd) {
       const uint32_t cnt = (uint32_t)__popcll(bm);
       if (cnt == 0) return;
       const bool mine = (bm >> lane) & 1ull;
-      const uint32_t id = mine ? nid[lane] : 0u;
-      const uint64_t key = mine ? make_key(nd[lane], id) : ~0ull;
+      const uint32_t id = mine ? cid : 0u;
+      const uint64_t key = mine ? make_key(cd, id) : ~0ull;
       if constexpr (!FULL) {
         if (mine) {
           vf_set(vf, vf_shift, id);
@@ -501,7 +498,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       while (r) {
         const int j = __ffsll((long long)r) - 1;
         r &= r - 1;
-        insert_key(__shfl(key, j, 64));
+        insert_key(readlane_u64(key, j));
       }
       const uint32_t tc = (uint32_t)__popcll(tm);
       if (tc) {
@@ -516,33 +513,33 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           while (r) {
             const int j = __ffsll((long long)r) - 1;
             r &= r - 1;
-            tail_insert(__shfl(key, j, 64));
+            tail_insert(readlane_u64(key, j));
           }
         }
         if (hn + ncq + nspill > maxq) maxq = hn + ncq + nspill;
       }
     };
-    // wave 0: accept `me` evaluated neighbours (nid[j], nd[j]) in neighbour
-    // order (Graph.cpp:471-483).  Only a candidate within the RESULT radius
-    // changes the state the next candidates see (it enters the results and
-    // may shrink both radii), so the candidates before the next such one are
-    // pushed as one batch, that one alone, and the rest re-tested against the
-    // new exploration radius -- the sequential order's outcome exactly.
-    auto accept = [&](uint32_t me) {
-      const float dl = (uint32_t)lane < me ? nd[lane] : 0.f;
-      const bool inl = (uint32_t)lane < me;
-      uint64_t okmask = ballot64(inl && dl <= expr);
+    // wave 0: accept the evaluated neighbours of the lanes in km (lane order
+    // = neighbour order; id and distance in cid / cd) as Graph.cpp:471-483
+    // does.  Only a candidate within the RESULT radius changes the state the
+    // next candidates see (it enters the results and may shrink both radii),
+    // so the candidates before the next such one are pushed as one batch,
+    // that one alone, and the rest re-tested against the new exploration
+    // radius -- the sequential order's outcome exactly.
+    auto accept = [&](uint64_t km, uint32_t cid, float cd) {
+      const bool inl = (km >> lane) & 1ull;
+      uint64_t okmask = ballot64(inl && cd <= expr);
       while (okmask) {
-        const uint64_t rmask = okmask & ballot64(inl && dl <= radius);
+        const uint64_t rmask = okmask & ballot64(inl && cd <= radius);
         if (rmask == 0ull) {
-          push_batch(okmask);
+          push_batch(okmask, cid, cd);
           break;
         }
         const int j = __ffsll((long long)rmask) - 1;
-        push_batch(okmask & ((1ull << j) - 1ull));
+        push_batch(okmask & ((1ull << j) - 1ull), cid, cd);
         // candidate j: d <= radius <= explorationRadius
-        const float d = nd[j];
-        const uint32_t id = nid[j];
+        const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cd), j));
+        const uint32_t id = (uint32_t)__builtin_amdgcn_readlane((int)cid, j);
         const uint64_t key = make_key(d, id);
         if constexpr (!FULL) {
           if (lane == 0) {
@@ -561,7 +558,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
         okmask &= ~((2ull << j) - 1ull);  // the candidates after j ...
-        okmask &= ballot64(inl && dl <= expr);  // ... within the (possibly smaller) radius
+        okmask &= ballot64(inl && cd <= expr);  // ... within the (possibly smaller) radius
       }
     };
 
@@ -726,7 +723,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
 #pragma unroll
           for (int j = 0; j < RG; j++) {
             const uint32_t e = base + 16u * j + (uint32_t)rs;
-            const uint32_t id = e < nl ? L[e] : 0u;
+            const uint32_t lv = L[e < nl ? e : 0u];  // unconditional: the reads issue together
+            const uint32_t id = e < nl ? lv : 0u;
             ids[j] = id;
             pw[j] = 0u;
             bit[j] = false;
@@ -736,14 +734,10 @@ ngt_graph_search_la_kernel(SearchArgs a) {
                 pw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
             }
+            // unconditional too (an empty entry reads object 0's codes)
             const uint2* cp = reinterpret_cast<const uint2*>(a.fcodes + (uint64_t)id * (4 * E)) + g * NW;
-            if (base + 16u * j < nl) {
 #pragma unroll
-              for (int w = 0; w < NW; w++) c[j][w] = cp[w];
-            } else {
-#pragma unroll
-              for (int w = 0; w < NW; w++) c[j][w] = make_uint2(0u, 0u);
-            }
+            for (int w = 0; w < NW; w++) c[j][w] = cp[w];
           }
 #pragma unroll
           for (int j = 0; j < RG; j++) {
@@ -948,14 +942,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
               ndist += (uint32_t)__popcll(ballot64(in && (!surv || keep)));
             }
             const uint64_t km = ballot64(keep);
-            if (keep) {
-              nid[mbcnt(km)] = id;
-              nd[mbcnt(km)] = xd;
-            }
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t me = (uint32_t)__popcll(km);
-            nexact += me;
-            if (me) accept(me);
+            nexact += (uint32_t)__popcll(km);
+            if (km) accept(km, id, xd);
             __builtin_amdgcn_wave_barrier();
           }
         }
