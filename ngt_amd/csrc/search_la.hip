@@ -642,7 +642,9 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       for (int jj = 0; jj < PW; jj++) {
         const uint32_t j = (uint32_t)(wave + W * jj);
         cnt[jj] = 0;
-        if (j < nt) load_adj_row(a.adj + (uint64_t)key_id(tkey[j]) * a.adj_stride, deg_cap, r[jj][0], r[jj][1],
+        // one wave: the targets are in its registers (no LDS round trip)
+        const uint64_t tkj = W == 1 ? tk[jj] : tkey[j < nt ? j : 0u];
+        if (j < nt) load_adj_row(a.adj + (uint64_t)key_id(tkj) * a.adj_stride, deg_cap, r[jj][0], r[jj][1],
                                  r[jj][2], r[jj][3]);
         else r[jj][0] = r[jj][1] = r[jj][2] = r[jj][3] = 0u;
       }
@@ -655,7 +657,11 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         if (j < nt && lane == 0) tcnt[j] = cnt[jj];
       }
       // the step hash starts empty
-      for (uint32_t i = tid; i < sh_n; i += NT) sh[i] = 0u;
+      if (sh_n % (4u * NT) == 0u) {
+        for (uint32_t i = 4u * tid; i < sh_n; i += 4u * NT) *reinterpret_cast<uint4*>(sh + i) = make_uint4(0, 0, 0, 0);
+      } else {
+        for (uint32_t i = tid; i < sh_n; i += NT) sh[i] = 0u;
+      }
       if constexpr (W > 1) __syncthreads();
       // list offsets: the targets whose lists fit the list capacity (t0 always does)
       uint32_t ntl = nt, tot = 0;
@@ -916,8 +922,10 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           for (uint32_t e0 = lb; e0 < le; e0 += 64) {
             const uint32_t e = e0 + (uint32_t)lane;
             const bool in = e < le;
-            const uint32_t id = in ? L[e] : 0u;
-            const uint32_t fl = in ? lfl[e] : 0u;
+            const uint32_t ec = in ? e : lb;  // unconditional reads, issued together
+            const uint32_t lv = L[ec], fv = lfl[ec];
+            const uint32_t id = in ? lv : 0u;
+            const uint32_t fl = in ? fv : 0u;
             bool keep;
             float xd = 0.f;
             if constexpr (FULL) {
@@ -937,7 +945,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
               // accepted before this step; the step's id set = accepted by
               // its earlier commits); every other entry counts as evaluated
               const bool surv = (fl & 2u) != 0u;
-              if (surv) xd = Xd[e];
+              xd = Xd[in ? e : lb];  // read for every lane: no dependent LDS round trip
               keep = surv && !(xd < 0.f) && (j == 0 ? true : !sh_contains(sh, a.la_sh_log2, id));
               ndist += (uint32_t)__popcll(ballot64(in && (!surv || keep)));
             }
