@@ -855,17 +855,18 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             xid[j] = id;
             xpw[j] = 0u;
             xchk[j] = false;
-            if constexpr (!FULL) {
-              // the survivor's visited test: LDS filter, then its HBM epoch
-              xchk[j] = g == 0 && rr < xtot && vf_test(vf, vf_shift, id);
-              if (xchk[j])
-                xpw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-            }
             const float4* x = reinterpret_cast<const float4*>(a.rows + (uint64_t)id * a.row_bytes) + g;
             if (j == 0 || r0 + 16u * j < xtot) {
 #pragma unroll
               for (int i = 0; i < NCH; i++) v[j][i] = x[4 * i];
+            }
+            if constexpr (!FULL) {
+              // the survivor's visited test: LDS filter, then its HBM epoch
+              // (after the row loads: they need not wait for the filter read)
+              xchk[j] = g == 0 && rr < xtot && vf_test(vf, vf_shift, id);
+              if (xchk[j])
+                xpw[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (id & ~3u)), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
             }
           }
 #pragma unroll
