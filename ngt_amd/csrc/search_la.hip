@@ -562,8 +562,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       }
     };
 
+    uint32_t fsq = 0;  // wave 0's copy (W == 1 reads it from registers)
     if (wave == 0) {
-      uint32_t fsq = 0;
       filter_query(qlds, a.dp, fa, fb, qb, fsq, frq);
       if (lane == 0) {
         ctl->fe = (double)a.fparams[2];
@@ -606,6 +606,8 @@ ngt_graph_search_la_kernel(SearchArgs a) {
     t_last = stamp();
 #endif
     for (;;) {
+      // wave 0's step control; with one wave it never goes through LDS
+      uint32_t s_done = 0, s_nt = 0, s_fthr = 0;
       // A. wave 0: the reference's next pop and the keys in line after it --
       // the nt <= P smallest keys of the unchecked set within the
       // exploration radius: the head's first lanes (refilled from the tail
@@ -623,17 +625,20 @@ ngt_graph_search_la_kernel(SearchArgs a) {
           for (int j = 0; j < P; j++)
             if ((uint32_t)j < nt) tkey[j] = tk[j];
         }
-        if (lane == 0) {
+        s_done = done;
+        s_nt = nt;
+        s_fthr = filter_threshold(expr, ctl->fe, ctl->finv_b, ctl->frq);
+        if (W > 1 && lane == 0) {
           ctl->done = done;
           ctl->nt = nt;
-          ctl->fthr = filter_threshold(expr, ctl->fe, ctl->finv_b, ctl->frq);
+          ctl->fthr = s_fthr;
         }
       }
       __syncthreads();
       NGT_MARK(t_a);
       nsteps++;
-      if (ctl->done) break;
-      const uint32_t nt = ctl->nt;
+      if (W == 1 ? s_done != 0u : ctl->done != 0u) break;
+      const uint32_t nt = W == 1 ? s_nt : ctl->nt;
 
       // B. adjacency rows of the targets (target j on wave j mod W), one round trip
       uint32_t r[PW][4];
@@ -713,11 +718,12 @@ ngt_graph_search_la_kernel(SearchArgs a) {
       NGT_MARK(t_b);
       const uint32_t nl = tot;
 
+      uint32_t xrun = 0;  // W == 1: survivors so far, entry order
       // C. visited-at-step-start test + filter codes of every list entry:
       // quad per entry, RG groups of 16 entries in flight per wave
       {
-        const uint32_t fthr = ctl->fthr, fsq = ctl->fsq;
-        uint32_t xrun = 0;  // W == 1: survivors so far, entry order
+        const uint32_t fthr = W == 1 ? s_fthr : ctl->fthr;
+        const uint32_t qsq = W == 1 ? fsq : ctl->fsq;
         uint2 q[NW];
         const uint2* qp = reinterpret_cast<const uint2*>(qb + g * E);
 #pragma unroll
@@ -756,7 +762,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
               cc = __builtin_amdgcn_udot4(c[j][w].x, c[j][w].x, cc, false);
               cc = __builtin_amdgcn_udot4(c[j][w].y, c[j][w].y, cc, false);
             }
-            const uint32_t S = fsq + quad_sum_u32(cc - 2u * qc);
+            const uint32_t S = qsq + quad_sum_u32(cc - 2u * qc);
             const uint32_t e = base + 16u * j + (uint32_t)rs;
             const uint32_t id = ids[j];
 #ifdef NGT_AMD_LACOUNT
@@ -780,18 +786,15 @@ ngt_graph_search_la_kernel(SearchArgs a) {
             }
           }
         }
-        if constexpr (W == 1) {
-          if (lane == 0) ctl->nx = xrun;
-        }
       }
       __syncthreads();
 
       // D. survivors (keep bits) of every target, in target then neighbour
       // order (one wave: collected in phase C already)
-      const uint32_t ntl_s = ctl->ntl;
+      const uint32_t ntl_s = ntl;  // every wave computed it from the same counts
       uint32_t xtot = 0;
       if constexpr (W == 1) {
-        xtot = ctl->nx;
+        xtot = xrun;
       } else {
       uint32_t xc[PW];
 #pragma unroll
@@ -958,11 +961,12 @@ ngt_graph_search_la_kernel(SearchArgs a) {
         }
         ndisc += ntl_s - ncommit;
         // the targets the commit did not reach are still in the head
-        if (done && lane == 0) ctl->done = 1;
+        s_done = done;
+        if (W > 1 && done && lane == 0) ctl->done = 1;
       }
       __syncthreads();
       NGT_MARK(t_f);
-      if (ctl->done) break;
+      if (W == 1 ? s_done != 0u : ctl->done != 0u) break;
     }
 
     // ---- results (moveFrom: ascending (distance, id), ObjectSpace.h:49-57)
