@@ -1035,7 +1035,7 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
 #define LA_T(NCH, PW)                                                                                           \
   do {                                                                                                          \
     if (la_wpe() == 4) {                                                                                        \
-      if (full) LA(NCH, 1, PW, 4, 1, true, 4); else LA(NCH, 1, PW, 4, 1, false, 4);                             \
+      if (full) LA(NCH, 1, PW, 3, 1, true, 4); else LA(NCH, 1, PW, 3, 1, false, 4);                             \
     } else {                                                                                                    \
       if (full) LA(NCH, 1, PW, 6, 1, true, 3); else LA(NCH, 1, PW, 6, 1, false, 3);                             \
     }                                                                                                           \
