@@ -1,5 +1,5 @@
 #!/bin/bash
-# counter passes of the ANNG line (lookahead kernel, survivors-only visited test)
+# counter passes of the ANNG line (lookahead kernel)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r4u}; mkdir -p $O
 D=/tmp/anng_r4u
