@@ -1,5 +1,5 @@
 #!/bin/bash
-# lookahead kernel: survivors collected during the filter pass (one wave), list
+# lookahead kernel (register head of the unchecked set; survivors collected in the filter pass), list
 # offsets from registers -- parity, then the ANNG line's launch time
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r4y}; mkdir -p $O
