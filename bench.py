@@ -1314,6 +1314,9 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
         torch.cuda.synchronize()
         kms.append(shards[s]["ix"].last_search_kernel_ms())
     filtered = (not qgm) and ix0.last_search_filtered()
+    # the schedule budget of those launches (0: single dispatches)
+    budget = 0 if qgm else shards[S - 1]["ix"].last_search_budget()
+    split = None  # (the exact mode's filter-copy split is not kept per shard)
     if not qgm and args.visited == -2:
         # the reference's distinct distance counts (every evaluated id in the
         # visited set) for the algorithmic bytes; the results must not change
