@@ -1287,6 +1287,18 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
             break
         chosen = round(chosen * 1.02 + 1e-4, 5)
         rec = measure(chosen)
+    if args.pmc_launches:
+        # counter passes: exactly this many more steps of the timed
+        # configuration (S shard searches each), nothing else of the bench
+        for _ in range(args.pmc_launches):
+            run(chosen)
+            torch.cuda.synchronize()
+        if rank == 0:
+            print(json.dumps({"pmc_launches": args.pmc_launches, "shards_per_gpu": S, "epsilon": chosen,
+                              "recall_at_10": rec}), file=result_out, flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     for _ in range(max(1, args.warmup)):
         run(chosen)
     torch.cuda.synchronize()
