@@ -228,6 +228,8 @@ def main():
                     help="knn: exact kNN graph built in setup (out/in edges); anng: this library's own "
                          "ngt_create_index ANNG (GraphAndTreeIndex::createIndex on the device)")
     ap.add_argument("--anng-edges", type=int, default=10, help="--graph anng: edgeSizeForCreation (ngt create -E)")
+    ap.add_argument("--anng-batch", type=int, default=200,
+                    help="--graph anng: batchSizeForCreation (ngt create -b, Command.cpp:41; int16, Graph.h:517)")
     ap.add_argument("--anng-dir", type=str, default="",
                     help="--graph anng: keep the saved index here, or open it if an earlier run saved it")
     ap.add_argument("--edge-size", type=int, default=None,
@@ -326,8 +328,9 @@ def main():
         # construction, ngt_save_index), checked against the reference's own
         # build of the same data (tests/golden/c2_anng_ref.json), and searched
         # on the device index that handle serves (ngt_get_device_index)
-        if N > 2_000_000:
-            # an index too large to write in the reference's format per run:
+        if N > 2_000_000 or args.anng_batch != 200:
+            # an index too large to write in the reference's format per run (or
+            # one built with another `ngt create -b` than the reference check's):
             # the same device construction, driven in id ranges with progress
             ix, offsets, edges, tree, build_s, anng_check, cx = build_anng_device(args, torch, dev, rows, N, D,
                                                                                  es_prop, local)
@@ -574,7 +577,8 @@ def main():
             la_form, c[:, 3].mean(), ne.mean()))
     kernel_ms = float(np.mean(kms)) if kms else float("nan")
     graph = ("kNN%d out%d in%d max%d" % (args.knn, args.out_deg, args.in_deg, args.max_deg) if args.graph == "knn"
-             else "ANNG E%d (ngt_create_index on the device)" % args.anng_edges)
+             else "ANNG E%d (ngt_create_index on the device)" % args.anng_edges
+             + ("" if args.anng_batch == 200 else ", batchSizeForCreation %d" % args.anng_batch))
     if qgm:
         # B(q) = sum_exp ceil(deg/16)*16*(M/2) + deg*4 + (seeds + k*expansion)*Dp*4  
         me = (D + 1) // 2 * 2
@@ -906,7 +910,7 @@ def build_anng_device(args, torch, dev, rows, N, D, es_prop, local):
         if first == 1:
             import ctypes as _ct
             from ngt_amd._sigs import BuildParams
-            prm = BuildParams(args.anng_edges, es_prop, 200, args.seed_size, 0.1, 0)
+            prm = BuildParams(args.anng_edges, es_prop, args.anng_batch, args.seed_size, 0.1, 0)
             if ix.L.ngt_amd_build_begin(ix.h, _ct.byref(prm)) != 0:
                 raise SystemExit("bench: ngt_amd_build_begin failed")
         if ix.L.ngt_amd_build_insert(ix.h, first, min(N + 1, first + step)) != 0:
@@ -919,8 +923,8 @@ def build_anng_device(args, torch, dev, rows, N, D, es_prop, local):
     ix.set_graph(offs, ids)
     ix.set_tree(tree)
     ix.set_search_property(es_prop, 30, 20, args.seed_size, 0)
-    log("ANNG (E=%d) of %d objects built on the device in %.1f s; %d edges, mean degree %.1f" % (
-        args.anng_edges, N, build_s, len(ids), len(ids) / N))
+    log("ANNG (E=%d, batch %d) of %d objects built on the device in %.1f s; %d edges, mean degree %.1f" % (
+        args.anng_edges, args.anng_batch, N, build_s, len(ids), len(ids) / N))
     offsets = torch.from_numpy(offs.astype(np.int64)).to(dev)
     edges = torch.from_numpy(ids.astype(np.int32)).to(dev)
     return ix, offsets, edges, tree, build_s, {"reference": None, "built": "device, ngt_amd_build_insert in id ranges"}, None

@@ -54,6 +54,32 @@ def test_device_anng_matches_reference_graph_and_tree():
     ix.close()
 
 
+@pytest.mark.parametrize("batch", [1000, 5000])
+def test_device_anng_batch_size_matches_reference(batch):
+    """`ngt create -d 128 -o f -D 2 -b <batch>` (batchSizeForCreation,
+    Command.cpp:41, Index.cpp:1297): the same edge lists and DVP tree leaves as
+    the reference CLI's build (tests/golden/make_batch_goldens.py).  At 5000
+    the whole data set is one batch, so every edge comes from the batch's
+    pairwise distances (Index.cpp:690-703)."""
+    rows, valid = F.read_obj(os.path.join(GOLD, "c1_anng", "obj"), 128, np.float32)
+    gold = os.path.join(GOLD, "c1_anng_b%d" % batch)
+    ix = DeviceIndex("l2", "float", 128)
+    ix.set_objects(rows, valid)
+    (offs, ids, ds), tree = ix.build_anng(batch_size_for_creation=batch)
+    goffs, gids, gds = F.read_grp(os.path.join(gold, "grp"))
+    assert len(offs) == len(goffs)
+    for v in range(1, len(offs) - 1):
+        a, b = int(offs[v]), int(offs[v + 1])
+        c, d = int(goffs[v]), int(goffs[v + 1])
+        assert list(ids[a:b]) == list(gids[c:d]), ("node", v)
+        assert np.array_equal(ds[a:b].view(np.uint32), gds[c:d].view(np.uint32)), ("node", v)
+    gt = F.read_tre(os.path.join(gold, "tre"), 128, np.float32)
+    assert _first_diff(tree["leaf_off"], gt["leaf_off"]) is None, _first_diff(tree["leaf_off"], gt["leaf_off"])
+    assert _first_diff(tree["leaf_ids"], gt["leaf_ids"]) is None, _first_diff(tree["leaf_ids"], gt["leaf_ids"])
+    assert _first_diff(tree["in_child"][1:], gt["in_child"][1:]) is None
+    ix.close()
+
+
 def test_capi_create_index_byte_identical(tmp_path):
     """ngt_create_graph_and_tree + ngt_insert_index_as_float x 5000 +
     ngt_create_index + ngt_save_index == the reference's files."""
