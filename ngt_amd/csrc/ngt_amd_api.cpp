@@ -322,6 +322,7 @@ std::string ngt_amd::device_error_text(int flag) {
       "latency kernel: tail-to-spill threshold selection check",              // 32
       "latency kernel: spill refill selection check",                         // 64
       "latency kernel: head refill selection check",                          // 128
+      "NGTQG kernel: spill chunk minimum not found (invariant)",               // 256: qg_kernels.hip
   };
   std::string out;
   for (int b = 0; b < 31; b++) {
@@ -330,7 +331,7 @@ std::string ngt_amd::device_error_text(int flag) {
     char num[16];
     snprintf(num, sizeof num, "%d: ", 1 << b);
     out += num;
-    out += b < 8 ? names[b] : "unknown bit";
+    out += b < 9 ? names[b] : "unknown bit";
   }
   return out;
 }

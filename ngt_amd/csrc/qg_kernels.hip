@@ -709,6 +709,22 @@ __device__ __forceinline__ void qg_exact(const float* qlds, const QgSearchArgs& 
   }
 }
 
+// Minimum of spill chunk c (keys c*64 .. min(n, c*64+64)), wave-uniform.
+__device__ __forceinline__ uint64_t chunk_min(const uint64_t* spill, uint32_t c, uint32_t n) {
+  const uint32_t i = c * 64 + lane_id();
+  return wave_min_u64(i < n ? spill[i] : ~0ull);
+}
+
+// Every chunk minimum of an n-key spill (after a compaction or the seeds);
+// tmin <- the last chunk's.
+__device__ __forceinline__ void spill_rebuild(const uint64_t* spill, uint64_t* cmin, uint32_t n, uint64_t& tmin) {
+  tmin = ~0ull;
+  for (uint32_t c = 0; c < ((n + 63) >> 6); c++) {
+    tmin = chunk_min(spill, c, n);
+    if (lane_id() == 0) cmin[c] = tmin;
+  }
+}
+
 // NB > 0: id rows of up to 16*NB entries load together with all their code
 // blocks (ids_and_adc); NB = 0: ids, then the codes of the degree read.
 template <int PPL, int NCH, int NB>
@@ -740,7 +756,11 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
 
   const uint32_t slot = blockIdx.x;
   uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
+  // HBM spill of the unchecked set in chunks of 64 keys, each chunk's exact
+  // minimum after the key area: a pop reads the chunk minima, not every key
   uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
+  const uint32_t scap = (uint32_t)(((uint64_t)a.spill_cap * 64 / 65) & ~(uint64_t)63);
+  uint64_t* cmin = spill + scap;
   const uint32_t hcap = use_hash ? 1u << a.ht_log2 : 0u;
   const uint32_t hlimit = hcap - (hcap >> 2);
   const uint32_t npairs = a.Me >> 1;
@@ -768,6 +788,8 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
 
     bool bitmap_mode = !use_hash;
     uint32_t nvisited = 0, ncq = 0, nspill = 0, nres = 0, maxq = 0;
+    uint64_t tmin = ~0ull;                   // minimum of the last spill chunk
+    float cq_cut = -1.0f, sp_cut = -1.0f;   // expr of the last compactions
     uint64_t nadc = 0, nacc = 0, nexp = 0, nexact = 0, nblk = 0;
     uint64_t t_pop = 0, t_ids = 0, t_adc = 0, t_acc = 0, t_last = 0;
     (void)t_pop; (void)t_ids; (void)t_adc; (void)t_acc; (void)t_last;
@@ -810,6 +832,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         __syncthreads();
       }
     }
+    if (nspill) spill_rebuild(spill, cmin, nspill, tmin);
     if (nres >= size) radius = key_dist(st.res[size - 1]);
     float expr = __fmul_rn(a.coef, radius);
 
@@ -824,8 +847,8 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         const uint64_t key = st.cq[i];
         if (key < best) { best = key; bidx = i; }
       }
-      for (uint32_t i = lane; i < nspill; i += 64) {
-        const uint64_t key = spill[i];
+      for (uint32_t i = lane; i < ((nspill + 63) >> 6); i += 64) {
+        const uint64_t key = cmin[i];
         if (key < best) { best = key; bidx = i | 0x80000000u; }
       }
       const uint64_t wbest = wave_min_u64(best);
@@ -834,11 +857,39 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       const uint64_t owner = ballot64(best == wbest);
       const int olane = __ffsll((long long)owner) - 1;
       bidx = __shfl(bidx, olane, 64);
-      if (lane == 0) {
-        if (bidx & 0x80000000u) spill[bidx & 0x7fffffffu] = spill[nspill - 1];
-        else st.cq[bidx] = st.cq[ncq - 1];
+      if (bidx & 0x80000000u) {
+        // the minimum is in spill chunk c: find it, move the last key into its
+        // place, refresh the minima of the chunks that changed
+        const uint32_t c = bidx & 0x7fffffffu;
+        const uint32_t i = c * 64 + lane;
+        const uint64_t k = i < nspill ? spill[i] : ~0ull;
+        const uint64_t hit = ballot64(k == wbest);
+        if (hit == 0) {
+          if (lane == 0) atomicOr(a.error, 256);
+          break;
+        }
+        const uint32_t pos = c * 64 + (uint32_t)(__ffsll((long long)hit) - 1);
+        const uint32_t last = nspill - 1;
+        const uint64_t lastkey = shfl_u64(lane == 0 ? spill[last] : 0ull, 0);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0 && pos != last) spill[pos] = lastkey;
+        nspill = last;
+        const uint64_t mc = wave_min_u64(i < nspill ? (i == pos ? lastkey : k) : ~0ull);
+        if (lane == 0) cmin[c] = mc;
+        const uint32_t L = last >> 6;
+        uint64_t mL = mc;
+        if (L != c) {
+          mL = chunk_min(spill, L, nspill);
+          if (lane == 0) cmin[L] = mL;
+        }
+        if (nspill) {
+          const uint32_t lp = (nspill - 1) >> 6;
+          tmin = lp == c ? mc : (lp == L ? mL : chunk_min(spill, lp, nspill));
+        }
+      } else {
+        if (lane == 0) st.cq[bidx] = st.cq[ncq - 1];
+        ncq--;
       }
-      if (bidx & 0x80000000u) nspill--; else ncq--;
       nexp++;
       NGT_MARK(t_pop);
 
@@ -884,18 +935,29 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
           if (!(d <= expr)) continue;
           acc |= 1ull << j;
           const uint64_t key = make_key(d, st.nid[base + j]);
-          if (ncq >= a.cq_cap) {
+          // keys beyond expr can never be popped; expr only shrinks, so a
+          // compaction at an unchanged expr would drop nothing
+          if (ncq >= a.cq_cap && expr != cq_cut) {
             ncq = compact(st.cq, ncq, expr);
-            if (nspill) nspill = compact(spill, nspill, expr);
+            cq_cut = expr;
           }
           if (ncq < a.cq_cap) {
             if (lane == 0) st.cq[ncq] = key;
             ncq++;
           } else {
-            if (nspill >= a.spill_cap) {
+            if (nspill >= scap && expr != sp_cut) {
+              nspill = compact(spill, nspill, expr);
+              sp_cut = expr;
+              spill_rebuild(spill, cmin, nspill, tmin);
+            }
+            if (nspill >= scap) {
               if (lane == 0) atomicOr(a.error, 1);
             } else {
-              if (lane == 0) spill[nspill] = key;
+              tmin = (nspill & 63) == 0 ? key : (key < tmin ? key : tmin);
+              if (lane == 0) {
+                spill[nspill] = key;
+                cmin[nspill >> 6] = tmin;
+              }
               nspill++;
             }
           }

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r4zm}; mkdir -p $O
 B=${B:-8000}
-for N in 200000 ${N:-12500000}; do
+for N in ${NS:-200000 12500000}; do
   timeout -k 10 ${T:-960} python -u bench.py --mode qg --graph anng --n $N --anng-batch $B --steps 3 --warmup 1 \
     --cpu-seconds 10 --latency-queries 0 --anng-line off > $O/c5_onegraph_$N.json 2> $O/c5_onegraph_$N.log \
     || { tail -20 $O/c5_onegraph_$N.log; exit 1; }
