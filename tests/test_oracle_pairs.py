@@ -98,6 +98,26 @@ def test_fixtures_regenerate_from_reference(tmp_path):
             assert x.tobytes() == y.tobytes(), (name, k)
 
 
+@pytest.mark.skipif(not _ref_ready(), reason="needs /root/reference (development container only)")
+def test_batch_fixtures_regenerate_from_reference(tmp_path):
+    """make_batch_goldens.py re-runs the reference CLI (`ngt create -b 1000 /
+    5000`) and its grp/tre equal the committed c1_anng_b* fixtures."""
+    subprocess.check_call(["make", "-s", "-j8", "-f", "oracle/ref.mk"], cwd=ROOT, stdout=subprocess.DEVNULL)
+    out = tmp_path / "gold"
+    out.mkdir()
+    import shutil
+    shutil.copy(os.path.join(GOLD, "sift5k.npy"), str(out / "sift5k.npy"))
+    subprocess.check_call([sys.executable, os.path.join(GOLD, "make_batch_goldens.py"), "--out", str(out),
+                           "--work", str(tmp_path / "work")], cwd=ROOT, stdout=subprocess.DEVNULL)
+    for b in (1000, 5000):
+        for f in ("prf", "grp", "tre"):
+            a = open(os.path.join(GOLD, "c1_anng_b%d" % b, f), "rb").read()
+            assert a == open(str(out / ("c1_anng_b%d" % b) / f), "rb").read(), (b, f)
+    # a different batch size gives a different graph (the fixtures pin -b)
+    assert open(os.path.join(GOLD, "c1_anng_b1000", "grp"), "rb").read() != \
+        open(os.path.join(GOLD, "c1_anng", "grp"), "rb").read()
+
+
 @pytest.mark.parametrize("isa", ["v3", "v4"])
 def test_native_builds_agree(isa):
     """The vectorized OpenMP builds bench.py times as the CPU baseline
