@@ -208,9 +208,110 @@ def tune_epsilon(measure, target, eps_list=None, lo=0.0, hi=0.05, tol=0.0005, la
     return hi
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` run without a torch.distributed launcher: start N
+    fresh rank processes of this same command (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment), one per GPU.  This parent
+    never imports torch and never touches a GPU, and it does not exec: the
+    ranks are children, rank 0's JSON line is relayed to stdout and the exit
+    status is the first failing rank's (the others are then stopped)."""
+    import signal
+    import subprocess
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    import threading
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log("rank %d exited with %d; stopping the others" % (procs.index(p), code))
+                stop()
+        time.sleep(0.05)
+    reader.join(10)
+    out = b"".join(chunks).decode(errors="replace")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if rc == 0 and lines:
+        print(lines[-1], flush=True)
+    elif rc == 0:
+        log("rank 0 printed no result line")
+        rc = 1
+    return rc
+
+
+def dry_run(args, result_out):
+    """The launcher's contract without a GPU (tests/test_bench_launcher.py):
+    every rank joins a gloo group, runs --steps timed steps of rank-dependent
+    length between barriers, and rank 0 prints the line with the max over
+    ranks, the ranks seen and the per-rank times."""
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if os.environ.get("NGT_BENCH_DRYRUN_FAIL_RANK") == str(rank):
+        raise SystemExit("bench: dry run: rank %d fails on request" % rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ones = torch.ones(1)
+    dist.all_reduce(ones)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.01 * (rank + 1))
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ranks = [None] * world
+    dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(), "elapsed": elapsed,
+                                   "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": world * args.steps / float(t.item()), "unit": "steps/s",
+                          "n_gpus": int(ones.item()), "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": float(t.item()) / args.steps * 1e3, "ranks": ranks}),
+              file=result_out, flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--shard-n", type=int, default=1_250_000, help="shard line: objects per shard")
+    ap.add_argument("--shard-count", type=int, default=8, help="shard line: shards of the whole index")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: gloo ranks time rank-dependent sleeps (no search)")
+    ap.add_argument("--shard-line", choices=["auto", "on", "off"], default="auto",
+                    help="attach C4's 10M index sharded over the ranks (8/N shards of 1.25M per rank) as the "
+                         "'shard' key; auto = on for the default C2 run with more than one rank")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--mode", choices=["exact", "qg", "shard", "capi"], default="exact")
@@ -261,10 +362,17 @@ def main():
                     help="visited set: -2 HBM epochs of accepted ids, -1 HBM epochs of every evaluated id "
                          "(C2 visits ~1e5 ids/query), 0 LDS hash")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start the N ranks ourselves (before torch)
+        return launch_ranks(args)
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%s" % (args.gpus, os.environ.get("WORLD_SIZE")))
     # stdout carries exactly one JSON line: everything else written to fd 1
     # (RCCL's init banner, library chatter) goes to stderr
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if args.dry_run:
+        return dry_run(args, result_out)
     qgm = args.mode == "qg" or (args.mode == "shard" and args.qg)
     if args.edge_size is None:
         args.edge_size = -1 if args.graph == "anng" else 0
@@ -287,11 +395,18 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
+    n_ranks = 1
     if world > 1 or args.mode == "shard":
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        # n_gpus = the ranks that actually joined the RCCL group
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        n_ranks = int(t.item())
+        if n_ranks != args.gpus:
+            raise SystemExit("bench: %d ranks joined RCCL, --gpus %d" % (n_ranks, args.gpus))
 
     from ngt_amd.device import COUNTERS, SEED_GIVEN, SEED_TREE, DeviceIndex
     if args.mode == "capi":
@@ -599,6 +714,7 @@ def main():
     if not qgm and la_form >= 0:
         kname = "ngt_graph_search_la_kernel"  # the lookahead kernel (search_la.hip) ran the timed launches
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    literal = literal_bytes(c, dp, NQ, K, qgm, D)
     split = None
     if filtered and not qgm:
         # where the algorithmic bytes come from: the 1-byte filter copy (N x Dp
@@ -713,7 +829,7 @@ def main():
             "metric": metric_name,
             "value": qps,
             "unit": "queries/s",
-            "n_gpus": world,
+            "n_gpus": n_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -741,9 +857,19 @@ def main():
                        "distance_filter": ("1-byte filter copy (lower bound rejects neighbours outside the "
                                            "exploration radius; exact f32 rows for the rest)" if filtered else "none"),
                        "streams": nstreams},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "roofline": {"bound": "unmeasured", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes,
+                         "bytes_definition": ("the filtered kernel's own bytes: 1-byte filter rows of every distinct "
+                                              "neighbour + f32 rows of the survivors (DESIGN.md 4)" if filtered
+                                              else "SURVEY.md 8(d) B(q)"),
+                         # SURVEY.md 8(d)'s literal B(q) = U*Dp*4 + E*4 + Dp*4 + k*8: the reference
+                         # algorithm's bytes.  Over the kernel time it is an EFFECTIVE rate, which the
+                         # filter lets exceed the HBM peak (the kernel never reads most of those rows)
+                         "literal_bytes_per_launch": literal,
+                         "effective_gbs_literal": literal / (kernel_ms * 1e-3) / 1e9,
+                         "effective_frac_literal": literal / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                         "infinity_cache_resident_share": ic_share(split, alg_bytes),
                          # the same bytes over the whole step with launches overlapping on the streams
                          # (a single launch's last round of queries leaves the GPU part-empty)
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
@@ -791,14 +917,11 @@ def main():
                     "active_inst_any_frac": cn["SQ_ACTIVE_INST_ANY"] / w,
                     "SQ_INSTS_LDS": cn.get("SQ_INSTS_LDS"),
                     "trace_avg_kernel_ms": tentry.get("trace_avg_kernel_ms")})
-                # what bounds the kernel, from the wave-cycle partition: more
-                # than half the wave-cycles parked on s_waitcnt = the
-                # dependent-gather latency, not the bytes' rate
-                if cn["SQ_WAIT_ANY"] / w >= 0.5:
-                    line["roofline"]["bound"] = "latency"
-                    line["roofline"]["bound_note"] = (
-                        "wait_any_frac >= 0.5: dependent gathers, not HBM bandwidth; achieved/peak still against "
-                        "the 8 TB/s HBM figure")
+                # what bounds the kernel, from the wave-cycle partition
+                line["roofline"]["bound"] = bound_from_counters(cn)
+                line["roofline"]["bound_note"] = (
+                    "from the SQ wave-cycle partition (wait_any_frac >= 0.5: dependent gathers, not HBM "
+                    "bandwidth); achieved/peak still against the 8 TB/s HBM figure")
         if qgm:
             line["config"]["result_expansion"] = args.expansion
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
@@ -814,9 +937,69 @@ def main():
                                                and args.graph == "knn" and world == 1)
         if want_anng:
             line["anng"] = anng_child_line(args)
+    want_shard = args.shard_line == "on" or (args.shard_line == "auto" and args.mode == "exact" and not c3
+                                             and args.graph == "knn" and world > 1 and not args.pmc_launches)
+    if want_shard:
+        # C4: the same 10M index at every N -- 8 shards of
+        # 1.25M objects, 8/N of them on each rank, one RCCL all-gather per
+        # step, merged recall and an oracle parity sample (strong scaling:
+        # the index and the batch are fixed, the ranks share them)
+        ix.close()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        if dist is None:  # --shard-line on with one rank: a one-rank RCCL group
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        sargs = argparse.Namespace(**vars(args))
+        sargs.mode, sargs.qg, sargs.eps, sargs.n = "shard", False, "", args.shard_n
+        sargs.shards_per_gpu = max(1, args.shard_count // world)
+        sargs.steps = max(3, min(args.steps, 10))
+        sargs.warmup = 1
+        log("shard line: C4 as %d x %d shards of %d objects" % (world, sargs.shards_per_gpu, sargs.n))
+        t0 = time.time()
+        sl = shard_bench(sargs, torch, dist, dev, rank, world, local, None, False, emit=False)
+        if rank == 0:
+            sl.pop("sweep", None)
+            sl["scaling"] = "strong"
+            sl["wall_s"] = time.time() - t0
+            line["shard"] = sl
+    if rank == 0:
         print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def literal_bytes(c, dp, nq, k, qgm, dim):
+    """SURVEY.md 8(d)'s algorithmic bytes of the reference algorithm from the
+    counters of a full-visited-set run: exact B(q) = U*Dp*4 + E*4 + Dp*4 + k*8;
+    NGTQG B(q) = sum ceil(deg/16)*16*(M/2) + deg*4 + (seeds + k*expansion)*Dp*4."""
+    if qgm:
+        me = (dim + 1) // 2 * 2
+        return float(c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4 + nq * (dp * 4 + k * 8))
+    return float(c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + nq * (dp * 4 + k * 8))
+
+
+def ic_share(split, alg_bytes):
+    """Share of the algorithmic bytes that come from tables the 256 MiB
+    Infinity Cache can hold (the 1-byte filter copy at C2: 128 MB)."""
+    if not split or not split.get("filter_copy_fits_infinity_cache"):
+        return 0.0
+    return float(split["filter_copy_bytes"] / alg_bytes)
+
+
+def bound_from_counters(cn):
+    """What bounds the kernel, from the SQ wave-cycle partition
+    (MI355X_MICROARCH.md rocprofv3 PMC): more than half the wave-cycles parked
+    on s_waitcnt = dependent-gather latency; else VALU-issue bound if VALU
+    issues on more than half; else the memory system."""
+    w = cn["SQ_WAVE_CYCLES"]
+    if cn.get("SQ_WAIT_ANY", 0) / w >= 0.5:
+        return "latency"
+    if cn.get("SQ_ACTIVE_INST_VALU", 0) / w >= 0.5:
+        return "valu"
+    return "hbm"
 
 
 def anng_child_line(args):
@@ -1178,7 +1361,7 @@ def capi_bench(args, torch, dev, result_out):
     ix.close()
 
 
-def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
+def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm, emit=True):
     """C4's and C5's form: the object repository as
     world x S shards of --n objects, rank r holding shards r*S .. r*S+S-1
     (global ids offset by shard * n), every shard an independent index with
@@ -1357,10 +1540,13 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
     kernel_ms = float(np.mean(kms))
     per_launch = alg_bytes / S
     achieved = per_launch / (kernel_ms * 1e-3) / 1e9
+    literal = literal_bytes(c, dp, S * NQ, K, qgm, D) / S
 
     cpu = parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = shard_parity_sample(args, shards, qdev, seeds, chosen, res, qgm)
+    if not args.no_cpu:
+        # every rank checks its own shards against the oracle; with several
+        # ranks the candidates are all-gathered and every rank checks the merge
+        cpu, parity = shard_parity_sample(args, shards, qdev, seeds, chosen, res, qgm, dist=dist)
 
     if rank == 0:
         total = N * S * world
@@ -1375,7 +1561,8 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
                         "k=%d, one packed RCCL all-gather of per-shard top-k + device merge" % (
                             N * S, S, N, world, NQ, K))
         line = {
-            "metric": metric_name, "value": qps, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric_name, "value": qps, "unit": "queries/s", "n_gpus": dist.get_world_size() if dist is not None else 1,
+            "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": "f32" if not qgm else "u4-adc/u8-lut/f32-rerank",
@@ -1389,9 +1576,17 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
                        "parallelism": "shards x%d (%d per GPU, one stream each)" % (S * world, S),
                        "distance_computations_per_query_per_shard": float(c[:, 0].mean()),
                        "expansions_per_query_per_shard": float(c[:, 2].mean())},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "roofline": {"bound": "unmeasured", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": per_launch,
+                         "bytes_definition": ("the filtered kernel's own bytes (DESIGN.md 4)" if filtered
+                                              else "SURVEY.md 8(d) B(q)"),
+                         "literal_bytes_per_launch": literal,
+                         "effective_gbs_literal": literal / (kernel_ms * 1e-3) / 1e9,
+                         "effective_frac_literal": literal / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                         "infinity_cache_resident_share": (
+                             (c[:, 0] - c[:, 7]).sum() * dp / S / per_launch
+                             if filtered and (N + 1) * dp <= 256 * 2 ** 20 else 0.0),
                          "what": "one shard's search launch alone (mean over the %d local shards)" % S,
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
                          "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
@@ -1408,18 +1603,23 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm):
                                                and args.graph == "knn" and world == 1)
         if want_anng:
             line["anng"] = anng_child_line(args)
+        if not emit:
+            return line
         print(json.dumps(line), file=result_out, flush=True)
-    if dist is not None:
+    if dist is not None and emit:
         dist.destroy_process_group()
 
 
-def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):
+def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm, dist=None):
     """The first --shard-sample queries of the batch through the oracle on
     every shard (searchReadOnlyGraph restatement, or the NGTQG search from the
     oracle's own LUTs on the shard's codebooks), merged on the host by
     (distance, global id): ids and float bits must equal the device's merged
-    results (abort otherwise).  Its time is the CPU baseline of the whole
-    sharded index on the host's cores."""
+    results (abort otherwise).  With several ranks each rank runs the oracle
+    on its own shards, the candidate lists are all-gathered (one object
+    collective) and every rank checks the merge.  The oracle's time (the max
+    over ranks) is the CPU baseline of the whole sharded index on the hosts'
+    cores."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     K = args.k
@@ -1429,6 +1629,7 @@ def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):
     isa = O.host_isa()
     L = O.native_lib(isa)
     el = 0.0
+    # per query: (distance, global id, distance bits) of every local shard's results
     cand = [[] for _ in range(n)]
     for sh in shards:
         h_rows = sh["rows"].cpu().numpy()
@@ -1453,32 +1654,44 @@ def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm):
             oi, od, on, _ = O.search_batch("l2", h_rows, h_off, h_edges, h_q, seeds[:n], K, np.float32(eps),
                                            edge_size=0, threads=threads, L=L)
         el += time.perf_counter() - t0
+        bits = od.view(np.uint32)
         for q in range(n):
             for j in range(int(on[q])):
-                cand[q].append((float(od[q, j]), int(oi[q, j]) + sh["off"], od[q, j]))
+                cand[q].append((float(od[q, j]), int(oi[q, j]) + sh["off"], int(bits[q, j])))
         del h_rows, h_off, h_edges
+    world = 1 if dist is None else dist.get_world_size()
+    el_max, cores = el, threads
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, {"cand": cand, "el": el, "threads": threads})
+        cand = [[c for g in got for c in g["cand"][q]] for q in range(n)]
+        el_max = max(g["el"] for g in got)
+        cores = sum(g["threads"] for g in got)
     gi = merged[0][:n].cpu().numpy().view(np.uint32)
-    gd = merged[1][:n].cpu().numpy()
+    gd = merged[1][:n].cpu().numpy().view(np.uint32)
     gn = merged[2][:n].cpu().numpy()
     same = True
     for q in range(n):
         best = sorted(cand[q], key=lambda t: (t[0], t[1]))[:K]
-        if int(gn[q]) != len(best) or any(int(gi[q, j]) != b[1] or gd[q, j].view(np.uint32) != b[2].view(np.uint32)
+        if int(gn[q]) != len(best) or any(int(gi[q, j]) != b[1] or int(gd[q, j]) != b[2]
                                           for j, b in enumerate(best)):
             same = False
             log("shard parity: query %d differs" % q)
             break
-    parity = {"queries": n, "identical": same,
-              "checked": "merged ids and float32 distance bits vs the oracle on every shard + host merge"}
+    nsh = len(shards) * world
+    parity = {"queries": n, "identical": same, "shards": nsh,
+              "checked": "merged ids and float32 distance bits vs the oracle on every shard + host merge"
+                         + (" (each rank's shards on its own host cores, candidates all-gathered)" if world > 1
+                            else "")}
     if not same:
         raise SystemExit("bench: sharded results differ from the oracle: %s" % parity)
-    log("shard parity sample: %d queries identical to the oracle over %d shards (%.1f s on %d threads)" % (
-        n, len(shards), el, threads))
+    log("shard parity sample: %d queries identical to the oracle over %d shards (%.1f s on %d threads%s)" % (
+        n, nsh, el_max, cores, ", max over %d ranks" % world if world > 1 else ""))
     what = "NGTQG search restatement (oracle LUTs)" if qgm else "searchReadOnlyGraph restatement"
-    cpu = {"value": n / el, "unit": "queries/s", "cores": threads, "kind": "port",
-           "sample": "first %d queries over all %d local shards, oracle/ngt_oracle.c %s built -O3 -march=x86-64-%s, "
-                     "one query per thread per shard on %d threads, %.1f s; host: %s, %d CPUs" % (
-                         n, len(shards), what, isa, threads, el, model, ncpu)}
+    cpu = {"value": n / el_max, "unit": "queries/s", "cores": cores, "kind": "port",
+           "sample": "first %d queries over all %d shards, oracle/ngt_oracle.c %s built -O3 -march=x86-64-%s, "
+                     "one query per thread per shard on %d threads per rank x %d ranks, %.1f s (max over ranks); "
+                     "host: %s, %d CPUs" % (n, nsh, what, isa, threads, world, el_max, model, ncpu)}
     return cpu, parity
 
 
@@ -1677,4 +1890,4 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -205,6 +205,11 @@ float ngt_amd_last_search_kernel_ms(const ngt_amd_index *index);
  * counters [6] are then the exact distances of neighbours the filter bound
  * could not place outside the exploration radius, [7] the seed distances. */
 int ngt_amd_last_search_filtered(const ngt_amd_index *index);
+/* The device error word of the launch context of `stream` (created on first
+ * use, zeroed on that stream and waited for), read on that stream: the word a
+ * search on the stream would start from.  Diagnostic; 0 unless a search on
+ * the stream left an invariant bit set (device_error_text). */
+int ngt_amd_stream_error_word(ngt_amd_index *index, void *stream, int *word);
 /* Workgroups (resident one-wave query slots) of the last search launch: per-CU
  * occupancy x CUs for a full batch, bounded by the visited-scratch HBM budget. */
 uint32_t ngt_amd_last_search_slots(const ngt_amd_index *index);

@@ -80,6 +80,7 @@ def declare(L):
         "ngt_amd_srand": (None, [c_uint]),
         "ngt_amd_last_search_kernel_ms": (c_float, [vp]),
         "ngt_amd_last_search_slots": (c_uint32, [vp]),
+        "ngt_amd_stream_error_word": (c_int, [vp, vp, vp]),
         "ngt_amd_last_search_budget": (c_uint32, [vp]),
         "ngt_amd_last_search_filtered": (c_int, [vp]),
         "ngt_amd_build_begin": (c_int, [vp, POINTER(BuildParams)]),

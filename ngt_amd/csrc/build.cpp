@@ -93,7 +93,7 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
   if (prm->edge_size_for_creation <= 0 || prm->batch_size_for_creation <= 0)
     return fail("ngt_amd_build_begin: edge_size_for_creation and batch_size_for_creation must be > 0");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   delete ix->build;
   auto* b = new BuildState();
   ix->build = b;
@@ -133,7 +133,7 @@ extern "C" int ngt_amd_build_begin(ngt_amd_index* ix, const ngt_amd_build_params
 extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64_t end_id) {
   if (!ix || !ix->build) return fail("ngt_amd_build_insert: call ngt_amd_build_begin first");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   // the insertion searches never rebuild the padded adjacency this call keeps
   // changing: build_begin set max_degree = adj_stride, so the copy always
   // holds every edge they read
@@ -180,7 +180,7 @@ extern "C" int ngt_amd_build_insert(ngt_amd_index* ix, uint64_t first_id, uint64
   std::vector<uint32_t> h_tseeds((size_t)B * SS), h_tcnt(B), h_mi((size_t)B * K), h_mn(B);
   std::vector<float> h_md((size_t)B * K);
   // NGT_AMD_BUILD_PROFILE=1: per-stage wall time (stream synchronised at each mark)
-  const bool prof = getenv("NGT_AMD_BUILD_PROFILE") != nullptr;
+  const bool prof = ngt_amd::knob("NGT_AMD_BUILD_PROFILE") != nullptr;
   double st[6] = {0, 0, 0, 0, 0, 0};
   auto t_last = std::chrono::steady_clock::now();
   DevBuf<uint64_t> d_cnt;
@@ -437,7 +437,7 @@ extern "C" int ngt_amd_build_set_graph(ngt_amd_index* ix, const uint64_t* offset
   if (!ix || !ix->build || !offsets || graph_rows > ix->nrows) return fail("ngt_amd_build_set_graph: bad arguments");
   if (offsets[graph_rows] && (!ids || !dists)) return fail("ngt_amd_build_set_graph: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   BuildState& b = *ix->build;
   const uint64_t S = b.adj_stride;
   std::vector<uint32_t> adj((size_t)ix->nrows * S, 0u);

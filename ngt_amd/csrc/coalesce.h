@@ -21,6 +21,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "knobs.h"
+
 #include <condition_variable>
 #include <deque>
 #include <exception>
@@ -60,7 +62,7 @@ struct CoalesceReq {
 
 inline bool coalesce_enabled() {
   static const bool on = [] {
-    const char* v = getenv("NGT_AMD_COALESCE");
+    const char* v = ngt_amd::knob("NGT_AMD_COALESCE");
     return !(v && atoi(v) == 0);
   }();
   return on;
@@ -69,10 +71,9 @@ inline bool coalesce_enabled() {
 class Coalescer {
  public:
   explicit Coalescer(uint32_t dim) : dim_(dim) {
-    const char* v = getenv("NGT_AMD_COALESCE_LEADERS");
-    max_leaders_ = v ? (atoi(v) < 1 ? 1 : atoi(v)) : 2;
-    v = getenv("NGT_AMD_COALESCE_MAX");
-    max_batch_ = v ? (uint32_t)(atoi(v) < 1 ? 1 : atoi(v)) : 4096u;
+    // 2 leaders (4 or 8: 3.1k / 2.6k vs 5.6k QPS at 32 threads)
+    max_leaders_ = 2;
+    max_batch_ = 4096u;
   }
 
   // runner(key, queries [nq][dim], nq, batch) fills every request of the batch.

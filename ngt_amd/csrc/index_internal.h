@@ -257,7 +257,14 @@ struct ngt_amd_index {
   uint32_t spill_cap = 1u << 16;
   hipStream_t stream = nullptr;
   ngt_amd::BuildState* build = nullptr;    // ANNG construction (build.cpp)
-  ngt_amd::Server* serve = nullptr;        // resident single-query serving grid (serve.cpp)
+  std::atomic<ngt_amd::Server*> serve{nullptr};  // resident single-query serving grid (serve.cpp)
+  // serving-grid exclusion (serve.cpp): a mutator holds the index from before
+  // it touches a buffer until the change is complete; served calls register
+  // only if no hold began since they read the index's buffers
+  std::mutex serve_mu;
+  int serve_hold = 0;        // under serve_mu: mutations in progress
+  int serve_inflight = 0;    // under serve_mu: served calls past registration
+  uint64_t serve_gen = 0;    // under serve_mu: holds begun so far
   ~ngt_amd_index() {
     for (auto* c : ctxs) delete c;
     for (auto* c : calls) delete c;
@@ -304,9 +311,18 @@ int build_padded_adjacency(ngt_amd_index* ix, uint64_t need);
 uint64_t adjacency_need(const ngt_amd_index* ix, uint64_t es);
 // stop and free the serving grid (serve.cpp); no-op without one
 void serve_destroy(ngt_amd_index* ix);
-// stop the serving grid before the index's buffers change (waits for the
-// served calls in flight; new ones take the launch path meanwhile)
+// stop the serving grid before the index's buffers change: new served calls
+// take the launch path, the calls in flight finish, the grid leaves; the hold
+// lasts until serve_resume (ServeHold does both)
 void serve_quiesce(ngt_amd_index* ix);
+void serve_resume(ngt_amd_index* ix);
+struct ServeHold {
+  ngt_amd_index* ix;
+  explicit ServeHold(ngt_amd_index* i) : ix(i) { serve_quiesce(ix); }
+  ~ServeHold() { serve_resume(ix); }
+  ServeHold(const ServeHold&) = delete;
+  ServeHold& operator=(const ServeHold&) = delete;
+};
 // GraphIndex::getRandomSeeds (Index.h:775-801) over the library's rand() stream
 // (a fresh process's glibc sequence, ngt_amd_srand)
 std::vector<uint32_t> random_seed_lists(ngt_amd_index* ix, uint32_t nq, std::vector<uint64_t>& off);

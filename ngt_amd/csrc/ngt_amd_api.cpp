@@ -73,7 +73,7 @@ extern "C" int ngt_amd_index_create(ngt_amd_index** out, int device, int distanc
   ix->esize = object_type == 2 ? 4 : 1;
   ix->row_bytes = (uint64_t)ix->dp * ix->esize;
   // test hook: a tiny unchecked-set spill makes the overflow flag reachable
-  if (const char* v = getenv("NGT_AMD_SPILL_CAP")) ix->spill_cap = (uint32_t)std::max(1, atoi(v));
+  if (const char* v = ngt_amd::knob("NGT_AMD_SPILL_CAP")) ix->spill_cap = (uint32_t)std::max(1, atoi(v));
   ix->cu_count = prop.multiProcessorCount;
   ix->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
   ix->lds_per_block = prop.sharedMemPerBlock ? prop.sharedMemPerBlock : 64 * 1024;
@@ -107,7 +107,7 @@ extern "C" int ngt_amd_index_set_objects(ngt_amd_index* ix, const void* rows, ui
                                          const uint8_t* valid) {
   if (!ix || !rows || nrows == 0) return fail("ngt_amd_index_set_objects: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   HIP_OK(ix->rows.upload(static_cast<const uint8_t*>(rows), nrows * ix->row_bytes));
   ix->nrows = nrows;
   ix->rows_version++;
@@ -121,7 +121,7 @@ extern "C" int ngt_amd_index_set_objects(ngt_amd_index* ix, const void* rows, ui
 extern "C" int ngt_amd_index_set_objects_device(ngt_amd_index* ix, const void* d_rows, uint64_t nrows) {
   if (!ix || !d_rows || nrows == 0) return fail("ngt_amd_index_set_objects_device: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   ix->rows.release();
   ix->rows.p = (uint8_t*)d_rows;
   ix->rows.n = nrows * ix->row_bytes;
@@ -152,7 +152,7 @@ int ngt_amd::build_padded_adjacency(ngt_amd_index* ix, uint64_t need) {
   if (need == 0 || need > 256) return 0;
   if (ix->adj.p && ix->adj_stride >= need) return 0;
   const uint64_t stride = (need + 15) & ~15ull;
-  serve_quiesce(ix);  // a running grid reads the copy being replaced
+  ServeHold serve_hold(ix);  // a running grid reads the copy being replaced
   ix->adj.release();
   ix->adj_stride = 0;
   HIP_OK(ix->adj.alloc(ix->nrows * stride));
@@ -175,7 +175,7 @@ uint64_t ngt_amd::adjacency_need(const ngt_amd_index* ix, uint64_t es) {
 }
 
 static int reset_adjacency(ngt_amd_index* ix, const uint64_t* h_offsets) {
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   ix->max_degree = max_degree_of(h_offsets, ix->nrows);
   ix->adj.release();
   ix->adj_stride = 0;
@@ -195,7 +195,7 @@ extern "C" int ngt_amd_index_set_graph(ngt_amd_index* ix, const uint64_t* offset
     if (edges[i] == 0 || edges[i] >= ix->nrows)
       return fail("ngt_amd_index_set_graph: edge %llu -> %u out of range", (unsigned long long)i, edges[i]);
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   HIP_OK(ix->edge_off.upload(offsets, ix->nrows + 1));
   HIP_OK(ix->edges.upload(edges, nedges));
   ix->nedges = nedges;
@@ -208,7 +208,7 @@ extern "C" int ngt_amd_index_set_graph_device(ngt_amd_index* ix, const uint64_t*
                                               const uint32_t* d_edges, uint64_t nedges) {
   if (!ix || !d_offsets) return fail("ngt_amd_index_set_graph_device: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   ix->edge_off.release();
   ix->edges.release();
   ix->edge_off.p = const_cast<uint64_t*>(d_offsets);
@@ -229,7 +229,7 @@ extern "C" int ngt_amd_index_set_tree(ngt_amd_index* ix, const void* in_pivot, u
                                       uint32_t n_leaf, const uint32_t* leaf_ids, uint64_t n_leaf_ids) {
   if (!ix || children < 2 || !leaf_off) return fail("ngt_amd_index_set_tree: bad arguments");
   HIP_OK(hipSetDevice(ix->device));
-  serve_quiesce(ix);
+  ServeHold serve_hold(ix);
   HIP_OK(ix->in_pivot.upload(static_cast<const uint8_t*>(in_pivot), (size_t)n_internal * ix->row_bytes));
   HIP_OK(ix->in_child.upload(in_child, (size_t)n_internal * children));
   HIP_OK(ix->in_border.upload(in_border, (size_t)n_internal * (children - 1)));
@@ -376,11 +376,11 @@ void ngt_amd::release_call(ngt_amd_index* ix, CallCtx* c) {
 int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds, uint32_t nq, hipStream_t s) {
   uint32_t per_cu = (uint32_t)(ix->lds_per_cu / lds);
   static const uint32_t max_per_cu = [] {
-    const char* v = getenv("NGT_AMD_WAVES_PER_CU");
+    const char* v = ngt_amd::knob("NGT_AMD_WAVES_PER_CU");
     return v ? (uint32_t)std::max(1, std::min(32, atoi(v))) : 16u;
   }();
   static const double mem_frac = [] {
-    const char* v = getenv("NGT_AMD_VIS_MEM_FRAC");
+    const char* v = ngt_amd::knob("NGT_AMD_VIS_MEM_FRAC");
     return v ? std::max(0.01, std::min(0.9, atof(v))) : 0.45;
   }();
   if (per_cu > max_per_cu) per_cu = max_per_cu;
@@ -471,14 +471,14 @@ static int ensure_filter(ngt_amd_index* ix) {
 // length), =2 only latency.
 static int lookahead_mode(const ngt_amd_index* ix, const SearchArgs& a, const ngt_amd_search_params* prm,
                           uint32_t nq) {
-  const char* ev = getenv("NGT_AMD_LA");
+  const char* ev = ngt_amd::knob("NGT_AMD_LA");
   const int env = ev ? atoi(ev) : 3;
   if (env == 0) return -1;
   if (ix->metric != NGT_AMD_DISTANCE_L2 || ix->otype != NGT_AMD_OBJECT_FLOAT || (ix->dp != 128 && ix->dp != 96))
     return -1;
   if (!a.adj || a.adj_stride > 256) return -1;
   if (prm->distance_filter < 0) return -1;  // the lookahead kernel always filters
-  if (getenv("NGT_AMD_FILTER") && atoi(getenv("NGT_AMD_FILTER")) == 0) return -1;
+  if (ngt_amd::knob("NGT_AMD_FILTER") && atoi(ngt_amd::knob("NGT_AMD_FILTER")) == 0) return -1;
   const int mode = nq < 2u * (uint32_t)ix->cu_count ? 1 : 0;
   // a wave per query pays off on short lists (an NGT index at its
   // EdgeSizeForSearch of 40: ~4 lists per step); long lists (the C2 kNN graph,
@@ -492,7 +492,7 @@ static int lookahead_mode(const ngt_amd_index* ix, const SearchArgs& a, const ng
 
 // NGT_AMD_SCHED=0: every search one launch in query order
 static int sched_mode() {
-  const char* v = getenv("NGT_AMD_SCHED");
+  const char* v = ngt_amd::knob("NGT_AMD_SCHED");
   return v ? atoi(v) : 1;
 }
 
@@ -542,7 +542,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     a.adj = fits ? ix->adj.p : nullptr;
     a.adj_stride = fits ? ix->adj_stride : 0;
   }
-  if (const char* v = getenv("NGT_AMD_ADJ"))
+  if (const char* v = ngt_amd::knob("NGT_AMD_ADJ"))
     if (atoi(v) == 0) a.adj = nullptr;
   int la_mode = -1;
   a.queries = static_cast<const uint8_t*>(d_queries);
@@ -606,10 +606,10 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     }
   }
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
-  if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
-  if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
-  if (const char* v = getenv("NGT_AMD_ACCEPTED_ONLY")) a.accepted_only = atoi(v) != 0;
-  if (const char* v = getenv("NGT_AMD_VFILTER")) {
+  if (const char* v = ngt_amd::knob("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
+  if (const char* v = ngt_amd::knob("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+  if (const char* v = ngt_amd::knob("NGT_AMD_ACCEPTED_ONLY")) a.accepted_only = atoi(v) != 0;
+  if (const char* v = ngt_amd::knob("NGT_AMD_VFILTER")) {
     const int f = atoi(v);
     a.vf_log2 = f <= 0 ? 0u : (uint32_t)std::max(11, std::min(18, f));
   }
@@ -625,7 +625,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   // costs a second round trip.  NGT_AMD_FILTER=0/1 forces it off/on.
   {
     static const int force = [] {
-      const char* v = getenv("NGT_AMD_FILTER");
+      const char* v = ngt_amd::knob("NGT_AMD_FILTER");
       return v ? atoi(v) : -1;
     }();
     // L2 rows of 96/128 floats (integer bound, pipelined expansion) or
@@ -633,7 +633,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     const bool shape = ix->otype == NGT_AMD_OBJECT_FLOAT &&
                        ((ix->metric == NGT_AMD_DISTANCE_L2 && (ix->dp == 128 || ix->dp == 96)) ||
                         ((ix->metric == NGT_AMD_DISTANCE_COSINE || ix->metric == NGT_AMD_DISTANCE_ANGLE) &&
-                         ix->dp > 128 && ix->dp % 64 == 0 && !getenv("NGT_AMD_NO_STREAM")));
+                         ix->dp > 128 && ix->dp % 64 == 0 && !ngt_amd::knob("NGT_AMD_NO_STREAM")));
     const bool want = force >= 0 ? force != 0
                                  : (prm->distance_filter != 0 ? prm->distance_filter > 0
                                                               : nq >= 2u * (uint32_t)ix->cu_count);
@@ -652,7 +652,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   if (la_mode >= 0) {
     // one step's target lists (<= 256 ids each) and the exact per-step id set
     static const uint32_t env_lmax = [] {
-      const char* v = getenv("NGT_AMD_LA_LMAX");
+      const char* v = ngt_amd::knob("NGT_AMD_LA_LMAX");
       return v ? (uint32_t)std::max(256, std::min(8192, atoi(v))) : 0u;
     }();
     // list capacity: the targets' lists of the longest kind (t0's always fits)
@@ -676,8 +676,8 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       a.vf_log2 = 14;
       a.cq_cap = 256u;
     }
-    if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
-    if (const char* v = getenv("NGT_AMD_VFILTER"))
+    if (const char* v = ngt_amd::knob("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+    if (const char* v = ngt_amd::knob("NGT_AMD_VFILTER"))
       if (atoi(v) > 0) a.vf_log2 = (uint32_t)std::max(11, std::min(18, atoi(v)));
   }
 
@@ -697,7 +697,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   bool lat = false;
   if (la_mode == 1) {
     static const bool lat_on = [] {
-      const char* v = getenv("NGT_AMD_LAT");
+      const char* v = ngt_amd::knob("NGT_AMD_LAT");
       return !v || atoi(v) != 0;
     }();
     const uint32_t cap = (uint32_t)std::min<uint64_t>(a.adj_stride, a.edge_size);
@@ -708,8 +708,8 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       while (search_lat_lds_bytes(b) > lds_max && b.lat_tail > 512u) b.lat_tail -= 256u;
       while (search_lat_lds_bytes(b) > lds_max && b.lat_slots > 8u) b.lat_slots -= 2u;
       // test knobs: a small tail forces the HBM spill, few slots the orphan path
-      if (const char* v = getenv("NGT_AMD_LAT_TAIL")) b.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
-      if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) b.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
+      if (const char* v = ngt_amd::knob("NGT_AMD_LAT_TAIL")) b.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
+      if (const char* v = ngt_amd::knob("NGT_AMD_LAT_SLOTS")) b.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
       if (search_lat_lds_bytes(b) <= lds_max) {
         a = b;
         lat = true;
@@ -762,15 +762,32 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     for (auto& m : c->sched_mean)
       if (m.first == skey) mean = m.second;
     static const double frac = [] {
-      const char* v = getenv("NGT_AMD_SCHED_FRAC");
+      const char* v = ngt_amd::knob("NGT_AMD_SCHED_FRAC");
       return v ? std::max(0.01, std::min(0.9, atof(v))) : 0.12;
     }();
     // test knob: a fixed budget for every eligible launch
-    const int forced = getenv("NGT_AMD_SCHED_B") ? std::max(0, atoi(getenv("NGT_AMD_SCHED_B"))) : 0;
+    const int forced = ngt_amd::knob("NGT_AMD_SCHED_B") ? std::max(0, atoi(ngt_amd::knob("NGT_AMD_SCHED_B"))) : 0;
     if (forced) budget = (uint32_t)forced;
     else if (mean > 0.0) budget = (uint32_t)std::max(8.0, mean * frac);
     // a tail needs more queries than slots (forced: any launch, for tests)
     if (!forced && (uint64_t)nq * 4 < (uint64_t)slots * 5) budget = 0;
+  }
+  if (budget) {
+    // the paused queries' records (~17 KB per query at cq_cap 1024) must fit
+    // beside everything else: at most a quarter of the free HBM, else (or if
+    // the allocation fails) the search is one dispatch -- same results
+    const PauseLayout lay(a.k, a.cq_cap, budget);
+    const size_t need = (size_t)nq * lay.total;
+    if (!(c->qstate.p && c->qstate.owned && c->qstate.n >= need)) {
+      size_t fr = 0, tot = 0;
+      HIP_OK(hipMemGetInfo(&fr, &tot));
+      const size_t bytes = need * sizeof(*c->qstate.p) + (size_t)nq * 16;
+      if (bytes > fr / 4 || c->qstate.alloc(need) != hipSuccess) {
+        (void)hipGetLastError();
+        c->qstate.release();
+        budget = 0;
+      }
+    }
   }
   c->launch_budget = budget;
   if (sched_shape) {
@@ -793,7 +810,6 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     HIP_OK(hipMemsetAsync(c->qflag.p, 0, (size_t)nq * sizeof(uint32_t), s));
     SearchArgs p = a;
     p.pause_after = budget;
-    p.sched_prio = getenv("NGT_AMD_SCHED_PRIO") ? (uint32_t)std::max(0, std::min(2, atoi(getenv("NGT_AMD_SCHED_PRIO")))) : 0u;
     p.qstate = c->qstate.p;
     p.qstate_stride = lay.total;
     p.qflag = c->qflag.p;
@@ -935,6 +951,17 @@ extern "C" uint32_t ngt_amd_last_search_budget(const ngt_amd_index* ix) {
   return c ? c->launch_budget : 0;
 }
 
+extern "C" int ngt_amd_stream_error_word(ngt_amd_index* ix, void* stream, int* word) {
+  if (!ix || !word) return fail("ngt_amd_stream_error_word: bad arguments");
+  HIP_OK(hipSetDevice(ix->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SearchCtx* c = ctx_for(ix, s);
+  if (!c) return -1;
+  HIP_OK(hipMemcpyAsync(word, c->err.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
 extern "C" uint32_t ngt_amd_last_search_slots(const ngt_amd_index* ix) {
   if (!ix) return 0;
   SearchCtx* c = ix->last_ctx.load();
@@ -1029,7 +1056,7 @@ extern "C" int ngt_amd_search(ngt_amd_index* ix, const ngt_amd_search_params* pr
 // normalization), plus the comparator's own rounding (rho) where used.
 static int scan_passes() {
   static const int p = [] {
-    const char* v = getenv("NGT_AMD_SCAN_PASSES");
+    const char* v = ngt_amd::knob("NGT_AMD_SCAN_PASSES");
     return v && atoi(v) == 1 ? 1 : 3;
   }();
   return p;
@@ -1110,17 +1137,10 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
   // Launches of at most one workgroup per CU.  Default: one launch, every
   // query block x floor(CUs / blocks) parts (a workgroup keeps its queries'
   // k-lists for its whole part; each part costs ~k ln(rows / k) candidates per
-  // query, so few long parts).  NGT_AMD_SCAN_XCD=1: launches of up to CUs / 8
-  // query blocks with 8 r parts, part p on XCD p % 8, so the workgroups that
-  // stream one part share that XCD's L2 (less fabric traffic, more parts).
+  // query, so few long parts).
   const uint32_t ntiles = (uint32_t)((ix->nrows + 255) / 256);
-  static const bool xcd = [] {
-    const char* v = getenv("NGT_AMD_SCAN_XCD");
-    return v && atoi(v) != 0;
-  }();
-  const uint32_t per_launch = xcd ? std::max(1, ix->cu_count / 8) : mblocks;
+  const uint32_t per_launch = mblocks;
   auto parts_of = [&](uint32_t mbc) -> uint32_t {
-    if (xcd) return 8 * std::max<uint32_t>(1, per_launch / mbc);
     uint32_t np = std::max<uint32_t>(1, (uint32_t)ix->cu_count / mbc);
     np = std::min(np, ntiles);
     const uint32_t per = (ntiles + np - 1) / np;
@@ -1163,8 +1183,8 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
       memcpy(&m.t_init, &u, 4);
     }
   }
-  if (const char* v = getenv("NGT_AMD_SCAN_DBG")) m.dbg = (uint32_t)atoi(v);
-  static const bool stats = getenv("NGT_AMD_SCAN_STATS") != nullptr;
+  if (const char* v = ngt_amd::knob("NGT_AMD_SCAN_DBG")) m.dbg = (uint32_t)atoi(v);
+  static const bool stats = ngt_amd::knob("NGT_AMD_SCAN_STATS") != nullptr;
   static DevBuf<unsigned long long> d_stats;
   if (stats) {
     HIP_OK(d_stats.alloc(4));
@@ -1183,7 +1203,7 @@ static int linear_search_mfma(ngt_amd_index* ix, SearchCtx* c, LinearArgs& a, hi
   }
   HIP_OK(c->partial.alloc(partial_total));
   size_t poff = 0;
-  m.xcd = xcd ? 1 : 0;
+  m.xcd = 0;
   for (uint32_t mb0 = 0; mb0 < mblocks; mb0 += per_launch) {
     const uint32_t mbc = std::min(per_launch, mblocks - mb0);
     const uint32_t nqc = std::min<uint32_t>(a.nq - mb0 * 128, mbc * 128);
@@ -1243,7 +1263,7 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
   // (scan_mfma.hip) -- bf16 MFMA dot products with a proven error bound pick
   // the candidates, the comparator recomputes them bit for bit.
   static const bool use_mfma = [] {
-    const char* v = getenv("NGT_AMD_LINEAR_MFMA");
+    const char* v = ngt_amd::knob("NGT_AMD_LINEAR_MFMA");
     return !(v && atoi(v) == 0);
   }();
   if (use_mfma && nq >= 32 && ix->otype == NGT_AMD_OBJECT_FLOAT && k <= 16 &&
@@ -1253,7 +1273,7 @@ extern "C" int ngt_amd_linear_search_device(ngt_amd_index* ix, const void* d_que
   // packed FMA, scan_kernels.hip) over enough row parts for ~3 workgroups
   // per CU slot; small batches keep the quad-per-row kernel below.
   static const bool tiled = [] {
-    const char* v = getenv("NGT_AMD_LINEAR_TILED");
+    const char* v = ngt_amd::knob("NGT_AMD_LINEAR_TILED");
     return !(v && atoi(v) == 0);
   }();
   if (tiled && nq >= 32 && ix->metric == NGT_AMD_DISTANCE_L2 && ix->otype == NGT_AMD_OBJECT_FLOAT && k <= 32 &&

@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "knobs.h"
+
 namespace ngt_amd {
 
 struct DistanceArgs {
@@ -112,8 +114,6 @@ struct SearchArgs {
   uint32_t* qflag;
   float* prio;
   unsigned long long* stat;      // [2]: expansions and queries finished by this launch (device sums) or null
-  uint32_t sched_prio;           // the probe's prediction: 0 unchecked keys within the exploration radius,
-                                 // 1 their margins sum (1 - d / radius_e), 2 keys within the result radius
 };
 
 // One paused query's saved state (the one-expansion kernel's accepted-only
@@ -194,23 +194,15 @@ struct ServeArgs {
 // per query), mode 1 (latency, eight waves per query)
 inline uint32_t la_targets(int mode) {
   if (mode != 0) return 8u;
-  // 2 (default: ANNG 88.4k QPS vs 72.5k at 3 and 57.8k at 4 targets per
-  // step, profiles/r3/anng_p), or NGT_AMD_LA_P = 1 / 3 / 4
-  const char* v = getenv("NGT_AMD_LA_P");
-  const int p = v ? atoi(v) : 2;
-  return p == 1 ? 1u : (p == 3 ? 3u : (p == 4 ? 4u : 2u));
+  // 2: ANNG 88.4k QPS vs 72.5k at 3 and 57.8k at 4 targets per step
+  // (profiles/r3/anng_p)
+  return 2u;
 }
 // resident waves per SIMD of the throughput form: 4 (128 VGPRs, 4 filter
 // groups in flight, 256 LDS keys, 16 Kbit filter: <= 10 KB of LDS so 16
 // workgroups fit a CU; ANNG 72.0k QPS) or 3 (168 VGPRs, 6 groups, 512 keys,
-// 32 Kbit; 64.7k QPS)
-inline int la_wpe() {
-  static const int w = [] {
-    const char* v = getenv("NGT_AMD_LA_WPE");
-    return v && atoi(v) == 3 ? 3 : 4;
-  }();
-  return w;
-}
+// 32 Kbit; 64.7k QPS): 4
+inline int la_wpe() { return 4; }
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 uint32_t search_lat_lds_bytes(const SearchArgs& a);
 hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStream_t s);
@@ -481,7 +473,6 @@ struct QgSearchArgs {
   uint32_t ht_log2;
   uint32_t cq_cap;
   uint32_t vf_log2;              // LDS visited-filter bits (log2); 0 = none
-  uint32_t two_trips;            // A/B switch: ids, then codes (no combined round trip)
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;
   uint32_t* out_n;

@@ -352,13 +352,12 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
     a.vf_log2 = 14;
   }
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
-  if (const char* v = getenv("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
-  if (const char* v = getenv("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
-  if (const char* v = getenv("NGT_AMD_VFILTER")) {
+  if (const char* v = ngt_amd::knob("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
+  if (const char* v = ngt_amd::knob("NGT_AMD_CQ_CAP")) a.cq_cap = (uint32_t)std::max(64, std::min(8192, atoi(v)));
+  if (const char* v = ngt_amd::knob("NGT_AMD_VFILTER")) {
     const int f = atoi(v);
     a.vf_log2 = f <= 0 ? 0u : (uint32_t)std::max(11, std::min(18, f));
   }
-  if (const char* v = getenv("NGT_AMD_QG_TWO_TRIPS")) a.two_trips = atoi(v) != 0;
   a.out_ids = d_ids;
   a.out_dists = d_dists;
   a.out_n = d_n;

@@ -898,7 +898,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       const uint32_t* nbr = a.qids + (uint64_t)target * a.id_stride;
       uint32_t deg = 0;
       uint64_t seen_pre[2] = {0, 0};
-      const bool early = NB > 0 && a.id_stride <= 16u * NB && !a.two_trips;
+      const bool early = NB > 0 && a.id_stride <= 16u * NB;
       const bool probe = early && !use_hash && st.vf != nullptr;
       if (early) {
         deg = ids_and_adc<PPL, (NB > 0 ? NB : 1)>(L, nbr, a.id_stride, a.qcodes + (uint64_t)target * a.code_stride,

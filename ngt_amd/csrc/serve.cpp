@@ -47,8 +47,8 @@ namespace {
 
 bool serve_enabled() {
   static const bool on = [] {
-    const char* v = getenv("NGT_AMD_SERVE");
-    const char* l = getenv("NGT_AMD_LAT");
+    const char* v = ngt_amd::knob("NGT_AMD_SERVE");
+    const char* l = ngt_amd::knob("NGT_AMD_LAT");
     return !(v && atoi(v) == 0) && !(l && atoi(l) == 0);
   }();
   return on;
@@ -96,8 +96,7 @@ struct Server {
   std::condition_variable tk_cv;
   uint32_t next = 0;
   std::vector<uint8_t> busy;
-  int inflight = 0;  // under mu
-  bool hold = false;  // under mu: the index is changing, callers take the launch path
+  int inflight = 0;  // under mu: calls on the grid's configuration (a switch waits for none)
   std::atomic<uint64_t> served{0}, launches{0};
   bool log = false;  // NGT_AMD_SERVE_LOG=1: a stderr line per grid
   std::chrono::steady_clock::time_point t_launch;
@@ -136,11 +135,11 @@ int server_init(ngt_amd_index* ix, Server* sv) {
   HIP_OK(sv->err.alloc(1));
   HIP_OK(hipMemsetAsync(sv->err.p, 0, sizeof(int), sv->s));
   HIP_OK(hipStreamSynchronize(sv->s));
-  const char* v = getenv("NGT_AMD_SERVE_WORKERS");
+  const char* v = ngt_amd::knob("NGT_AMD_SERVE_WORKERS");
   const int w = v ? atoi(v) : 128;
   sv->workers = (uint32_t)std::max(1, std::min(w, ix->cu_count - 1));
-  if (const char* t = getenv("NGT_AMD_SERVE_IDLE_MS")) sv->idle_ms = std::max(1.0, atof(t));
-  if (const char* t = getenv("NGT_AMD_SERVE_LOG")) sv->log = atoi(t) != 0;
+  if (const char* t = ngt_amd::knob("NGT_AMD_SERVE_IDLE_MS")) sv->idle_ms = std::max(1.0, atof(t));
+  if (const char* t = ngt_amd::knob("NGT_AMD_SERVE_LOG")) sv->log = atoi(t) != 0;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ix->device) == hipSuccess && khz > 0)
     sv->clock_khz = (uint64_t)khz;
@@ -252,8 +251,8 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   a.lat_tail = 4096u;
   while (search_lat_lds_bytes(a) > lds_max && a.lat_tail > 512u) a.lat_tail -= 256u;
   while (search_lat_lds_bytes(a) > lds_max && a.lat_slots > 8u) a.lat_slots -= 2u;
-  if (const char* v = getenv("NGT_AMD_LAT_TAIL")) a.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
-  if (const char* v = getenv("NGT_AMD_LAT_SLOTS")) a.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
+  if (const char* v = ngt_amd::knob("NGT_AMD_LAT_TAIL")) a.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
+  if (const char* v = ngt_amd::knob("NGT_AMD_LAT_SLOTS")) a.lat_slots = (uint32_t)std::max(2, std::min(64, atoi(v)));
   if (search_lat_lds_bytes(a) > lds_max) return 1;
   cfg = ServeConfig{};
   cfg.rows = ix->rows.p;
@@ -279,35 +278,45 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
 // The index is about to change (rows, graph, padded adjacency, tree): new
 // served calls take the launch path, the calls in flight finish, and the grid
 // leaves -- it holds the old buffers' pointers, and so does the relaunch
-// state sv->a.  The next served call relaunches with the index's new state.
+// state sv->a.  The hold lasts until serve_resume, i.e. until the mutator has
+// swapped its buffers: a served call that read the index before the hold
+// began sees serve_gen changed when it tries to register and takes the launch
+// path, so no grid or relaunch is ever configured with a freed pointer.
 // The callers in flight never take ix->mu, so a caller holding it may wait here.
 void serve_quiesce(ngt_amd_index* ix) {
-  Server* sv = ix->serve;
-  if (!sv) return;
-  for (bool first = true;; first = false) {
+  {
+    std::lock_guard<std::mutex> lk(ix->serve_mu);
+    ix->serve_hold++;
+    ix->serve_gen++;
+  }
+  for (;;) {
     {
-      std::lock_guard<std::mutex> lk(sv->mu);
-      if (first) sv->hold = true;
-      if (sv->inflight == 0) {
-        (void)server_reap(sv, true);
-        sv->cfg = ServeConfig{};
-        sv->hold = false;
-        return;
-      }
+      std::lock_guard<std::mutex> lk(ix->serve_mu);
+      if (ix->serve_inflight == 0) break;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
+  Server* sv = ix->serve.load();
+  if (!sv) return;
+  std::lock_guard<std::mutex> lk(sv->mu);
+  (void)server_reap(sv, true);
+  sv->cfg = ServeConfig{};
+}
+
+void serve_resume(ngt_amd_index* ix) {
+  std::lock_guard<std::mutex> lk(ix->serve_mu);
+  ix->serve_hold--;
 }
 
 void serve_destroy(ngt_amd_index* ix) {
-  Server* sv = ix->serve;
+  Server* sv = ix->serve.load();
   if (!sv) return;
   {
     std::lock_guard<std::mutex> lk(sv->mu);
     (void)server_reap(sv, true);
   }
   delete sv;
-  ix->serve = nullptr;
+  ix->serve.store(nullptr);
 }
 
 }  // namespace ngt_amd
@@ -318,6 +327,14 @@ extern "C" int ngt_amd_search_served(ngt_amd_index* ix, const ngt_amd_search_par
                                      uint32_t* ids, float* dists, uint32_t* n, uint64_t* counters) {
   if (!ix || !prm || !query || !ids || !dists || !n) return fail("ngt_amd_search_served: bad arguments");
   if (!serve_enabled()) return 1;
+  // the index's buffers are read below without a lock: valid only if no
+  // mutation (serve_quiesce .. serve_resume) began meanwhile
+  uint64_t gen0;
+  {
+    std::lock_guard<std::mutex> lk(ix->serve_mu);
+    if (ix->serve_hold) return 1;
+    gen0 = ix->serve_gen;
+  }
   SearchArgs a{};
   ServeConfig cfg{};
   {
@@ -328,20 +345,32 @@ extern "C" int ngt_amd_search_served(ngt_amd_index* ix, const ngt_amd_search_par
   Server* sv;
   {
     std::lock_guard<std::mutex> lk(ix->mu);
-    if (!ix->serve) {
+    if (!ix->serve.load()) {
       Server* fresh = new Server();
       if (server_init(ix, fresh)) {
         delete fresh;
         return -1;
       }
-      ix->serve = fresh;
+      ix->serve.store(fresh);
     }
-    sv = ix->serve;
+    sv = ix->serve.load();
   }
+  // register: from here a mutator's quiesce waits for this call
+  {
+    std::lock_guard<std::mutex> lk(ix->serve_mu);
+    if (ix->serve_hold || ix->serve_gen != gen0) return 1;
+    ix->serve_inflight++;
+  }
+  struct Unregister {
+    ngt_amd_index* ix;
+    ~Unregister() {
+      std::lock_guard<std::mutex> lk(ix->serve_mu);
+      ix->serve_inflight--;
+    }
+  } unregister{ix};
   // join the grid's configuration, or switch it when nothing is in flight
   {
     std::lock_guard<std::mutex> lk(sv->mu);
-    if (sv->hold) return 1;
     if (!(sv->cfg == cfg)) {
       if (sv->inflight > 0) return 1;
       if (server_reap(sv, true)) return -1;
@@ -452,7 +481,8 @@ extern "C" int ngt_amd_serve_stop(ngt_amd_index* ix) {
 extern "C" int ngt_amd_serve_stats(ngt_amd_index* ix, uint64_t* served, uint64_t* launches) {
   if (!ix || !served || !launches) return fail("ngt_amd_serve_stats: bad arguments");
   std::lock_guard<std::mutex> lk(ix->mu);
-  *served = ix->serve ? ix->serve->served.load() : 0;
-  *launches = ix->serve ? ix->serve->launches.load() : 0;
+  Server* sv = ix->serve.load();
+  *served = sv ? sv->served.load() : 0;
+  *launches = sv ? sv->launches.load() : 0;
   return 0;
 }

@@ -55,8 +55,14 @@ extern "C" int ngt_amd_shard_comm_create(ngt_amd_shard_comm** out, int device, i
   c->device = device;
   c->rank = rank;
   c->world = world;
-  if (c->err.alloc(1) != hipSuccess || hipMemsetAsync(c->err.p, 0, sizeof(int), nullptr) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
+  // the error word is zeroed on a stream of its own and only that stream is
+  // waited for: a device-wide synchronize would also wait for a resident
+  // serving grid (serve.cpp), which leaves only after its idle time
+  hipStream_t zs = nullptr;
+  bool ok = c->err.alloc(1) == hipSuccess && hipStreamCreateWithFlags(&zs, hipStreamNonBlocking) == hipSuccess &&
+            hipMemsetAsync(c->err.p, 0, sizeof(int), zs) == hipSuccess && hipStreamSynchronize(zs) == hipSuccess;
+  if (zs) (void)hipStreamDestroy(zs);
+  if (!ok) {
     delete c;
     return fail("ngt_amd_shard_comm_create: allocation failed");
   }

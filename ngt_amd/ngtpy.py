@@ -8,6 +8,8 @@ id array with ``with_distance=False``, ids zero-based unless
 libngt_amd.so (``ngt_batch_search_index`` / ``_using_only_graph`` /
 ``ngt_batch_linear_search_index``); there is no host fallback.
 """
+import os
+
 import numpy as np
 
 from . import NativeError
@@ -29,6 +31,48 @@ def create(path, dimension, edge_size_for_creation=10, edge_size_for_search=40, 
     base.Index.create(path, dimension, edge_size_for_creation, edge_size_for_search, ot, distance_type)
 
 
+def accuracy_table(path):
+    """The prf's AccuracyTable (Index.h:255, written by the optimizer) as
+    Index::AccuracyTable::set parses it (Index.h:299-315): comma-separated
+    ``epsilon:accuracy`` pairs, epsilon stored as float, accuracy as double;
+    fewer than two tokens leave the table empty."""
+    text = ""
+    with open(os.path.join(path, "prf")) as f:
+        for line in f:
+            key, _, val = line.rstrip("\n").partition("\t")
+            if key == "AccuracyTable":
+                text = val
+    toks = [t for t in text.split(",") if t]
+    if len(toks) < 2:
+        return []
+    table = []
+    for t in toks:
+        ts = [x for x in t.split(":") if x]
+        if len(ts) != 2:
+            raise NativeError("AccuracyTable: Invalid accuracy table string %s:%s" % (t, text))
+        table.append((np.float32(float(ts[0])), float(ts[1])))
+    return table
+
+
+def epsilon_from_expected_accuracy(table, accuracy):
+    """Index::AccuracyTable::getEpsilon (Index.h:317-346): linear
+    interpolation between the entries that bracket `accuracy`, in the
+    reference's mixed float/double arithmetic, clamped below at -0.9."""
+    if len(table) <= 2:
+        raise NativeError("AccuracyTable: The accuracy table is not set yet. The table size=%d" % len(table))
+    accuracy = min(float(accuracy), 1.0)
+    i = 0
+    while i < len(table) and table[i][1] < accuracy:
+        i += 1
+    if i == len(table):
+        i -= 2
+    elif i != 0:
+        i -= 1
+    (lf, ls), (uf, us) = table[i], table[i + 1]
+    e = np.float32(float(lf) + float(np.float32(uf - lf)) * (accuracy - ls) / (us - ls))
+    return float(max(e, np.float32(-0.9)))
+
+
 class Index(object):
     """ngtpy.Index (ngtpy.cpp:30-50): defaults k=20, epsilon=0.1,
     radius=FLT_MAX, edge size from the property."""
@@ -43,7 +87,9 @@ class Index(object):
         self.epsilon = 0.1
         self.radius = FLT_MAX
         self.edge_size = -1
+        self.expected_accuracy = -1.0  # defaultExpectedAccuracy (ngtpy.cpp:49)
         self.distance_computations = 0
+        self._table = None
 
     def _id_out(self, ids):
         return ids.astype(np.int64) - 1 if self.zero else ids.astype(np.int64)
@@ -59,17 +105,26 @@ class Index(object):
 
     def search(self, query, size=0, epsilon=-FLT_MAX, edge_size=INT_MIN, expected_accuracy=-FLT_MAX,
                with_distance=True):
-        """ngtpy.cpp:141-214: tree-seeded search unless tree_disabled."""
-        if expected_accuracy > 0.0:
-            raise NativeError("ngtpy::search: expected_accuracy needs the optimizer's accuracy table "
-                              "(graph tooling, out of scope); pass epsilon")
+        """ngtpy.cpp:141-214: tree-seeded search unless tree_disabled.  A
+        positive expected_accuracy replaces epsilon with the one the prf's
+        AccuracyTable maps it to (sc.setExpectedAccuracy, then
+        GraphIndex::search's getEpsilonFromExpectedAccuracy, Index.h:1156-1158)."""
         q = np.ascontiguousarray(query, dtype=np.float32).reshape(1, -1)
         k = size if size > 0 else self.num_of_search_objects
         eps = self.epsilon if epsilon <= -1.0 else epsilon
+        if expected_accuracy > 0.0:
+            eps = self.epsilon_for(expected_accuracy)
         es = self.edge_size if edge_size < -2 else edge_size
         ids, ds, n = self._ix.batch_search(q, k, eps, self.radius, es, graph_only=not self.tree)
         self.distance_computations += int(self._ix.last_search_counters()[0])
         return self._results(ids, ds, n, with_distance)
+
+    def epsilon_for(self, expected_accuracy):
+        """The epsilon a search with this expected accuracy uses (the pybind
+        argument is a float, widened to double for getEpsilon)."""
+        if self._table is None:
+            self._table = accuracy_table(self._ix.path)
+        return epsilon_from_expected_accuracy(self._table, float(np.float32(expected_accuracy)))
 
     def linear_search(self, query, size=0, with_distance=True):
         """ngtpy.cpp:216-268: exact k-NN by full scan within the index's search
@@ -86,7 +141,10 @@ class Index(object):
 
     def set(self, num_of_search_objects=0, search_radius=-FLT_MAX, epsilon=-FLT_MAX, edge_size=INT_MIN,
             expected_accuracy=-FLT_MAX):
-        """ngtpy.cpp:322-333: a non-positive / out-of-range value keeps the default."""
+        """ngtpy.cpp:322-333: a non-positive / out-of-range value keeps the
+        default.  expected_accuracy is kept as defaultExpectedAccuracy, which
+        the reference's search never reads (it takes only its own argument,
+        ngtpy.cpp:168-172): a set() value changes no search there or here."""
         if num_of_search_objects > 0:
             self.num_of_search_objects = num_of_search_objects
         if epsilon > -1.0:
@@ -95,6 +153,8 @@ class Index(object):
             self.radius = search_radius
         if edge_size >= -2:
             self.edge_size = edge_size
+        if expected_accuracy > 0.0:
+            self.expected_accuracy = expected_accuracy
 
     def insert(self, object, debug=False):
         """ngtpy.cpp:119-139: append one object (no graph update until build_index)."""

@@ -19,7 +19,7 @@ CXXFLAGS = -Ofast -march=native -fopenmp -std=c++17 -fPIC -w -I$(GEN) -I$(GEN)/N
 SRCS = $(wildcard $(REF)/lib/NGT/*.cpp) $(wildcard $(REF)/lib/NGT/NGTQ/*.cpp)
 OBJS = $(patsubst $(REF)/lib/%.cpp,$(OUT)/obj/%.o,$(SRCS))
 
-all: $(OUT)/libngt_ref.so $(OUT)/ngt $(OUT)/ngtq $(OUT)/ngtqg $(OUT)/qg_harness $(OUT)/ngtq_harness $(OUT)/comparator_harness $(OUT)/kmeans_harness
+all: $(OUT)/libngt_ref.so $(OUT)/ngt $(OUT)/ngtq $(OUT)/ngtqg $(OUT)/qg_harness $(OUT)/ngtq_harness $(OUT)/comparator_harness $(OUT)/kmeans_harness $(OUT)/accuracy_harness
 
 $(GEN)/NGT/defines.h: $(REF)/lib/NGT/defines.h.in oracle/configure_defines.cmake
 	@mkdir -p $(GEN)/NGT
@@ -60,3 +60,6 @@ $(OUT)/ngtq_harness: tests/golden/ngtq_harness.cpp $(OUT)/libngt_ref.so
 
 $(OUT)/kmeans_harness: tests/golden/kmeans_harness.cpp ngt_amd/csrc/kmeans_ngt.h $(OUT)/libngt_ref.so
 	$(CXX) $(CXXFLAGS) -Ingt_amd/csrc -o $@ $< -L$(OUT) -lngt_ref -Wl,-rpath,$(abspath $(OUT))
+
+$(OUT)/accuracy_harness: tests/golden/accuracy_harness.cpp $(OUT)/libngt_ref.so
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lngt_ref -Wl,-rpath,$(abspath $(OUT))

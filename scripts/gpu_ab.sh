@@ -2,6 +2,7 @@
 # A/B of two library builds on the ANNG line (interleaved runs, one built graph):
 #   scripts/gpu_ab.sh <out> <libA> <libB> [rounds]
 set -o pipefail
+export NGT_AMD_TEST_KNOBS=1  # the library reads NGT_AMD_* knobs only with this set (csrc/knobs.h)
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/$1; mkdir -p $O
 D=/tmp/anng_ab
 timeout -k 10 400 python3 -u bench.py --graph anng --anng-dir $D --eps 0.1279296875 --sweep-nq 10000 --steps 1 --warmup 1 \

@@ -2,6 +2,7 @@
 # A/B of two library builds on the C2 headline (interleaved, 20 overlapped steps each)
 #   scripts/gpu_ab_c2.sh <out> <libA> <libB> [rounds]
 set -o pipefail
+export NGT_AMD_TEST_KNOBS=1  # the library reads NGT_AMD_* knobs only with this set (csrc/knobs.h)
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/$1; mkdir -p $O
 for r in $(seq 1 ${4:-2}); do for v in A B; do
   L=$2; [ $v = B ] && L=$3

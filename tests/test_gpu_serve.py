@@ -7,6 +7,7 @@ batch launch's counters, for tree seeds (GraphAndTreeIndex::getSeedsFromTree
 on the device, Index.h:1524-1567) and random seeds (getRandomSeeds, the same
 rand() stream as a launch), under concurrency, with the HBM spill and slot
 reaping forced, and across a change of the index (the grid relaunches)."""
+import ctypes
 import os
 import threading
 
@@ -160,3 +161,98 @@ def test_served_follows_index_changes():
     gi2, _, _ = ix.search_served(q, k=10, epsilon=0.1)  # relaunched after the stop
     assert list(gi2) == list(gi)
     ix.close()
+
+
+def test_fresh_stream_error_word_zero_under_resident_grid():
+    """GPUTEST_r03's "flag 36": a fresh call stream's launch context once read
+    a stale error word because its zero-fill went to the null stream and sat
+    behind the resident grid.  While served calls keep the grid resident,
+    every new stream's word must read 0 before its first launch, and a batch
+    search on it must succeed."""
+    import torch
+    ix, rows, offs, ids, tree = _anng(n=3000, seed=7)
+    rng = np.random.default_rng(5)
+    qs = rng.random((8, rows.shape[1]), dtype=np.float32)
+    assert ix.search_served(qs[0], k=10, epsilon=0.1) is not None
+    stop = threading.Event()
+    errors = []
+
+    def keep_resident():
+        try:
+            i = 0
+            while not stop.is_set():
+                ix.search_served(qs[i % len(qs)], k=10, epsilon=0.1)
+                i += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=keep_resident)
+    th.start()
+    try:
+        dev = torch.device("cuda", 0)
+        dq = torch.from_numpy(np.ascontiguousarray(qs)).to(dev)
+        for _ in range(6):
+            st = torch.cuda.Stream(dev)
+            w = ctypes.c_int(-1)
+            assert ix.L.ngt_amd_stream_error_word(ix.h, st.cuda_stream, ctypes.byref(w)) == 0
+            assert w.value == 0
+            oi = torch.zeros((len(qs), 10), dtype=torch.int32, device=dev)
+            od = torch.zeros((len(qs), 10), dtype=torch.float32, device=dev)
+            on = torch.zeros((len(qs),), dtype=torch.int32, device=dev)
+            ix.search_device(dq.data_ptr(), dq.shape[1] * 4, len(qs), oi.data_ptr(), od.data_ptr(), on.data_ptr(),
+                             k=10, epsilon=0.1, seed_mode=SEED_TREE, stream=st.cuda_stream)
+            st.synchronize()
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors[:3]
+    ix.close()
+
+
+def test_index_changes_under_concurrent_served_calls():
+    """a served call that read the index before a mutation began
+    must not configure or relaunch the grid with the old buffers.  Four
+    threads post served queries while the main thread replaces the graph
+    (which releases and rebuilds the padded adjacency) and the tree, over and
+    over, with identical contents: every answer, served or not, equals the
+    oracle's."""
+    ix, rows, offs, ids, tree = _anng(n=3000, seed=9)
+    rng = np.random.default_rng(6)
+    qs = rng.random((16, rows.shape[1]), dtype=np.float32)
+    es = ix.resolve_edge_size(-1, 0.1)
+    want = [_oracle(rows, offs, ids, tree, q, 10, 0.1, es) for q in qs]
+    stop = threading.Event()
+    errors, served = [], [0]
+
+    def worker(t):
+        try:
+            i = t
+            while not stop.is_set():
+                r = ix.search_served(qs[i % len(qs)], k=10, epsilon=0.1)
+                if r is not None:
+                    oi, od, _ = want[i % len(qs)]
+                    if list(r[0]) != list(oi) or not np.array_equal(r[1].view(np.uint32), od.view(np.uint32)):
+                        errors.append("query %d differs" % (i % len(qs)))
+                    served[0] += 1
+                i += 4
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    try:
+        for _ in range(12):
+            ix.set_graph(offs, ids)
+            ix.set_tree(tree)
+    finally:
+        stop.set()
+        for t in th:
+            t.join()
+    assert not errors, errors[:3]
+    assert served[0] > 0
+    bi, bd, bn, _ = ix.search(qs, k=10, epsilon=0.1, seed_mode=SEED_TREE)
+    for i in range(len(qs)):
+        assert list(bi[i, :bn[i]]) == list(want[i][0]), i
+    ix.close()
+
