@@ -358,6 +358,12 @@ def main():
     ap.add_argument("--anng-line", choices=["auto", "on", "off"], default="auto",
                     help="attach the NGT-built index's line (a child run of --graph anng) as the 'anng' key; "
                          "auto = on for the default single-GPU C2 run")
+    ap.add_argument("--capi-line", choices=["auto", "on", "off"], default="auto",
+                    help="with --graph anng: the drop-in C API (ngt_open_index + ngt_search_index from a pthreads C "
+                         "client) on the same saved index as the 'capi' key; auto = on for the 1M ANNG")
+    ap.add_argument("--c3-line", choices=["auto", "on", "off"], default="auto",
+                    help="attach C3 (1M x 960 cosine, a child run of --config c3) as the 'c3' key; auto = on for "
+                         "the default single-GPU C2 run")
     ap.add_argument("--visited", type=int, default=-2,
                     help="visited set: -2 HBM epochs of accepted ids, -1 HBM epochs of every evaluated id "
                          "(C2 visits ~1e5 ids/query), 0 LDS hash")
@@ -377,7 +383,9 @@ def main():
     if args.edge_size is None:
         args.edge_size = -1 if args.graph == "anng" else 0
     if args.seeds is None:
-        args.seeds = "tree" if args.graph == "anng" and not qgm else "random"
+        # an index with a DVP tree seeds from it: GraphAndTreeIndex::search and
+        # NGTQG::Index::search (QuantizedGraph.h:354-372) alike
+        args.seeds = "tree" if args.graph == "anng" else "random"
     es_prop = 40 if args.graph == "anng" else 0  # the prf's EdgeSizeForSearch (Command.cpp:40)
     if qgm and args.visited == -2:
         args.visited = -1  # the QG search marks accepted ids only by definition (QuantizedGraph.h:241-266)
@@ -436,6 +444,15 @@ def main():
     build_s = None
     tree = None
     anng_check = None
+    capi_dir = None
+    if (args.graph == "anng" and world == 1 and not args.pmc_launches and N == 1_000_000 and D == 128
+            and args.anng_batch == 200 and (args.capi_line == "on" or args.capi_line == "auto")):
+        # the C-API line opens the index this run saves (ngt_save_index) from disk
+        import tempfile
+        if not args.anng_dir:
+            capi_dir = args.anng_dir = tempfile.mkdtemp(prefix="ngt_anng_capi_")
+        else:
+            capi_dir = args.anng_dir
     if args.graph == "anng":
         # the index a user of `ngt create -d 128 -o f -D 2 -E <e>` gets, built
         # through the drop-in C API (ngt_create_graph_and_tree,
@@ -535,8 +552,10 @@ def main():
         ix.qg_encode(return_codes=False)
         ix.qg_build_graph(None, args.qg_edges)
         torch.cuda.synchronize()
-        log("quantizer (kmeansWithNGT, %d subspaces) %.1f s + encoder + quantized graph %.1f s (degree <= %d)" % (
-            D, t1 - t0, time.time() - t1, ix.qg_max_degree()))
+        qg_record_bytes = int(ix.L.ngt_amd_qg_record_bytes(ix.h))
+        log("quantizer (kmeansWithNGT, %d subspaces) %.1f s + encoder + quantized graph %.1f s (degree <= %d); "
+            "packed search layout %.2f GB (%.0f B per node)" % (D, t1 - t0, time.time() - t1, ix.qg_max_degree(),
+                                                               qg_record_bytes / 1e9, qg_record_bytes / max(1, N)))
 
     def run(eps, si=0, visited=None, nq=NQ):
         oi, od, on, oc = bufs[si]
@@ -800,6 +819,12 @@ def main():
     ref_check = None
     if rank == 0 and anng_check is not None and anng_check.get("reference"):
         ref_check = reference_fixture_check(ix, qdev, dp, K, dev, torch)
+    capi = None
+    if rank == 0 and capi_dir:
+        capi = capi_anng_line(capi_dir, qry, gt, D, K, chosen, args.threads)
+        if not (args.anng_dir and args.anng_dir != capi_dir):
+            import shutil
+            shutil.rmtree(capi_dir, ignore_errors=True)
 
     if rank == 0:
         if args.mode == "exact" and not c3 and N > 2_000_000:
@@ -894,6 +919,8 @@ def main():
             line["config"]["reference_search_check"] = ref_check
         if latency is not None:
             line["single_query_latency"] = latency
+        if capi is not None:
+            line["capi"] = capi
         cn = tentry.get("counters_per_launch")
         if cn:
             # PMC evidence for what bounds the kernel (profiles/traffic.json):
@@ -924,6 +951,11 @@ def main():
                     "bandwidth); achieved/peak still against the 8 TB/s HBM figure")
         if qgm:
             line["config"]["result_expansion"] = args.expansion
+            line["config"]["qg_layout"] = (
+                {"packed_record_bytes": qg_record_bytes, "bytes_per_node": qg_record_bytes / N,
+                 "what": "per node ceil(deg/16) code blocks of 8*Me bytes + 16 {id, key word} entries per block "
+                         "(QuantizedGraph.h:74-113's per-node blocks); a popped key names its record and length"}
+                if qg_record_bytes else {"fixed_stride_code_bytes_per_node": int(ix.L.ngt_amd_qg_code_stride(ix.h))})
             line["config"]["adc_distances_per_query"] = float(c[:, 0].mean())
             line["config"]["accepted_per_query"] = float(c[:, 1].mean())
             line["config"]["exact_distances_per_query"] = float(c[:, 3].mean())
@@ -937,6 +969,11 @@ def main():
                                                and args.graph == "knn" and world == 1)
         if want_anng:
             line["anng"] = anng_child_line(args)
+        want_c3 = args.c3_line == "on" or (args.c3_line == "auto" and args.mode == "exact" and not c3
+                                           and args.graph == "knn" and world == 1 and N == 1_000_000
+                                           and not args.pmc_launches)
+        if want_c3:
+            line["c3"] = c3_child_line(args)
     want_shard = args.shard_line == "on" or (args.shard_line == "auto" and args.mode == "exact" and not c3
                                              and args.graph == "knn" and world > 1 and not args.pmc_launches)
     if want_shard:
@@ -1031,6 +1068,68 @@ def anng_child_line(args):
     log("ANNG line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
         d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
     return d
+
+
+def c3_child_line(args):
+    """C3 (BASELINE config 3: 1M x 960 float cosine, kNN graph, the cosine
+    filter) measured beside the headline: a child process of this bench
+    (`--config c3`) with its own roofline, cpu_baseline and parity sample;
+    None if it fails."""
+    import subprocess
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", "c3", "--anng-line", "off", "--c3-line", "off",
+           "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1", "--cpu-seconds", str(min(args.cpu_seconds, 10.0)),
+           "--latency-queries", "0"]
+    if args.no_cpu:
+        cmd.append("--no-cpu")
+    t0 = time.time()
+    log("C3 line: %s" % " ".join(cmd[2:]))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=env, timeout=900)
+    out = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not out:
+        log("C3 line failed (rc %d)" % r.returncode)
+        return {"error": "child run failed", "rc": r.returncode}
+    d = json.loads(out[-1])
+    d.pop("sweep", None)
+    d["child_wall_s"] = time.time() - t0
+    log("C3 line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
+        d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
+    return d
+
+
+def capi_anng_line(index_dir, Q, gt, D, K, eps, threads):
+    """The drop-in C API on the 1M ANNG this run built and saved: a pthreads
+    C client (tests/cxx/capi_threads.c) opens the directory with
+    ngt_open_index and issues single-query ngt_search_index calls
+    (Capi.cpp:377-406) -- 1 thread (latency), `threads` and 2x `threads`
+    concurrent callers at the bench's epsilon -- and, for parity, the
+    reference fixture's 200 queries at its epsilon on one thread: the ids
+    must equal `ngt search`'s own output on the reference's build of the same
+    data (tests/golden/c2_anng_ref.npz)."""
+    t0 = time.time()
+    runs = capi_c_client(index_dir, Q, gt, D, K, eps, threads)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c2_anng_ref.npz"))
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "c2_anng_ref.json")))
+    n = z["ids"].shape[0]
+    eps_ref = float(meta["sweep"]["epsilon"])
+    ref_runs = capi_c_client(index_dir, Q[:n], gt[:n], D, K, eps_ref, 1, plan=[(1, n)], keep_ids=True)
+    got = ref_runs[0].pop("ids")
+    same = all(np.array_equal(got[q, :int(z["n"][q])], z["ids"][q, :int(z["n"][q])].astype(got.dtype))
+               and not got[q, int(z["n"][q]):].any() for q in range(n))
+    best = max(runs, key=lambda r: r["qps"])
+    one = [r for r in runs if r["threads"] == 1][0]
+    out = {"what": "ngt_open_index + single-query ngt_search_index calls from a pthreads C client "
+                   "(tests/cxx/capi_threads.c) on the saved 1M ANNG (tree seeds, the prf's edge size 40)",
+           "epsilon": eps, "single_thread_latency_ms": one["latency_ms"], "qps_best": best["qps"],
+           "threads_best": best["threads"], "runs": runs,
+           "reference_parity": {"queries": n, "epsilon": eps_ref, "ids_identical_to_ngt_search": bool(same),
+                                "recall_at_10_vs_truth": ref_runs[0]["recall_at_10"]},
+           "wall_s": time.time() - t0}
+    log("C API on the ANNG: 1 thread %.2f ms/query, best %.0f QPS at %d threads; reference ids identical: %s" % (
+        one["latency_ms"]["mean"], best["qps"], best["threads"], same))
+    return out
 
 
 def measured_traffic(mode, config, graph, eps, visited, filtered=False):
@@ -1695,7 +1794,7 @@ def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm, dist=None):
     return cpu, parity
 
 
-def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
+def capi_c_client(index_dir, Q, gt, D, K, eps, threads, plan=None, keep_ids=False):
     """tests/cxx/capi_threads.c compiled here with gcc against include/ and
     libngt_amd.so, run as a child process on the index directory: sequential
     single-query latency, `threads` concurrent callers and twice as many.
@@ -1710,7 +1809,7 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
     qpath = os.path.join(index_dir, "queries.f32")
     np.ascontiguousarray(Q, np.float32).tofile(qpath)
     out = []
-    for t, calls in [(1, 300), (threads, 200), (2 * threads, 150)]:
+    for t, calls in plan or [(1, 300), (threads, 200), (2 * threads, 150)]:
         ids_path = os.path.join(index_dir, "ids.u32")
         env = dict(os.environ)
         r = subprocess.run([exe, index_dir, qpath, str(Q.shape[0]), str(D), str(K), repr(float(eps)), str(t),
@@ -1723,6 +1822,8 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads):
         ids = np.fromfile(ids_path, np.uint32).reshape(-1, K).astype(np.int64)
         qi = np.arange(ids.shape[0]) % Q.shape[0]
         res["recall_at_10"] = recall_at(ids, gt[qi], K)
+        if keep_ids:
+            res["ids"] = ids
         out.append(res)
         log("C client: %d threads: %.0f QPS, latency mean %.3f ms p99 %.3f, recall %.4f (%d grid launches)" % (
             t, res["qps"], res["latency_ms"]["mean"], res["latency_ms"]["p99"], res["recall_at_10"],

@@ -388,6 +388,11 @@ int ngt_amd_qg_set_graph(ngt_amd_index *index, const uint64_t *qoff, const uint3
 uint32_t ngt_amd_qg_max_degree(const ngt_amd_index *index);
 /* Bytes of one node's code row (max degree / 16 blocks of 8 * Me bytes). */
 uint64_t ngt_amd_qg_code_stride(const ngt_amd_index *index);
+/* Bytes of the packed search layout of the quantized graph (per node its
+ * ceil(degree/16) code blocks and their {id, key word} entries, the reference's
+ * per-node layout of QuantizedGraphRepository, QuantizedGraph.h:74-113), or 0
+ * when searches read the fixed-stride slabs. */
+uint64_t ngt_amd_qg_record_bytes(const ngt_amd_index *index);
 /* Copy the quantized graph back to the host (what QuantizedGraphRepository::
  * serialize writes, QuantizedGraph.h:117-128): ids [nrows][max_degree]
  * (0-terminated) and codes [nrows][code_stride] in the reference stream layout. */

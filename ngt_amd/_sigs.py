@@ -111,6 +111,7 @@ def declare(L):
         "ngt_amd_qg_set_graph": (c_int, [vp, vp, vp, vp, vp]),
         "ngt_amd_qg_max_degree": (c_uint32, [vp]),
         "ngt_amd_qg_code_stride": (c_uint64, [vp]),
+        "ngt_amd_qg_record_bytes": (c_uint64, [vp]),
         "ngt_amd_qg_get_graph": (c_int, [vp, vp, vp]),
         "ngt_amd_qg_lut": (c_int, [vp, vp, c_uint32, vp, vp, vp]),
         "ngt_amd_qg_adc": (c_int, [vp, vp, vp, vp, c_uint32, vp, vp, c_uint64, vp, vp]),

@@ -70,6 +70,15 @@ struct QgState {
   uint32_t id_stride = 0;
   uint64_t code_stride = 0;
   bool has_graph = false;
+  // the search layout (qg_pack): one record per node in id order, its code
+  // blocks then 16 entries {id, key word} per block; a node's key word is
+  // (record unit << 3) | (blocks - 1), so a popped key names the record and
+  // its length and both load in one round trip (qg_api.cpp, qg_kernels.hip)
+  DevBuf<uint8_t> recs;     // sum over nodes of blocks * (8*Me + 128) bytes, rounded to 1 << rec_shift
+  DevBuf<uint32_t> qkw;     // [nrows] key word of every node (0 for the dummy)
+  uint32_t rec_shift = 0;
+  uint64_t rec_bytes = 0;
+  bool packed = false;
 };
 
 // NGTQ IVF-ADC quantizer attached to a global-codebook index (ivf_api.cpp)

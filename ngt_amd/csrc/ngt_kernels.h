@@ -473,6 +473,9 @@ struct QgSearchArgs {
   uint32_t ht_log2;
   uint32_t cq_cap;
   uint32_t vf_log2;              // LDS visited-filter bits (log2); 0 = none
+  const uint8_t* recs;           // packed records (QgState::recs), or null: the fixed-stride slabs
+  const uint32_t* qkw;           // [nrows] key words of the packed layout
+  uint32_t rec_shift;            // record unit = 1 << rec_shift bytes
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;
   uint32_t* out_n;
@@ -488,6 +491,12 @@ struct QgSearchArgs {
 
 hipError_t launch_qg_lut(const QgLutArgs& a, hipStream_t s);
 hipError_t launch_qg_build(const QgBuildArgs& a, hipStream_t s);
+// packed search layout: blocks per node (>= 1) from the fixed id rows, then
+// every node's record and key word (QgState::recs / qkw)
+hipError_t launch_qg_blocks(const uint32_t* qids, uint32_t id_stride, uint32_t nrows, uint8_t* nb, hipStream_t s);
+hipError_t launch_qg_pack(const uint32_t* qids, uint32_t id_stride, const uint8_t* qcodes, uint64_t code_stride,
+                          uint32_t Me, uint32_t nrows, const uint32_t* qkw, uint32_t rec_shift, uint8_t* recs,
+                          hipStream_t s);
 hipError_t launch_qg_adc(const QgAdcArgs& a, hipStream_t s);
 hipError_t launch_qg_encode(const QgEncodeArgs& a, hipStream_t s);
 hipError_t launch_qg_train(const QgTrainArgs& a, hipStream_t s);

@@ -42,6 +42,9 @@ extern "C" int ngt_amd_qg_set_quantizer(ngt_amd_index* ix, const float* global, 
   if (q.M != M) {
     q.qids.release();
     q.qcodes.release();
+    q.recs.release();
+    q.qkw.release();
+    q.packed = false;
     q.has_graph = false;
   }
   q.M = M;
@@ -114,6 +117,63 @@ extern "C" int ngt_amd_qg_train(ngt_amd_index* ix, uint32_t M, uint32_t nsample,
   return ngt_amd_qg_set_quantizer(ix, zero.data(), h.data(), M, dsub);
 }
 
+// The packed search layout (qg_kernels.hip): blocks per node on the device,
+// record units and key words on the host (a prefix sum in id order), then the
+// records.  Used when the search kernel variant holds a whole node's blocks
+// (<= 8 with one LUT pair per lane, <= 4 with two) and 2^29 record units of
+// at most 4 KiB cover the graph; otherwise searches read the fixed slabs.
+static int qg_pack(ngt_amd_index* ix) {
+  QgState& q = ix->qg;
+  q.packed = false;
+  q.recs.release();
+  q.qkw.release();
+  q.rec_bytes = 0;
+  const uint32_t pairs = q.Me / 2;
+  const uint32_t nbmax = pairs <= 64 ? 8u : (pairs <= 128 ? 4u : 0u);
+  if (q.id_stride / 16 > nbmax) return 0;
+  if (const char* v = ngt_amd::knob("NGT_AMD_QG_PACKED"))
+    if (atoi(v) == 0) return 0;
+  const uint64_t n = ix->nrows;
+  DevBuf<uint8_t> dnb;
+  HIP_OK(dnb.alloc(n));
+  HIP_OK(launch_qg_blocks(q.qids.p, q.id_stride, (uint32_t)n, dnb.p, ix->stream));
+  std::vector<uint8_t> nb(n);
+  HIP_OK(hipMemcpyAsync(nb.data(), dnb.p, n, hipMemcpyDeviceToHost, ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  const uint64_t rec_per_block = (uint64_t)8 * q.Me + 128;  // codes + 16 entries of 8 bytes
+  uint32_t shift = 7;
+  uint64_t units = 0;
+  for (; shift <= 12; shift++) {
+    units = 0;
+    for (uint64_t v = 1; v < n; v++) units += (nb[v] * rec_per_block + (1ull << shift) - 1) >> shift;
+    if (units < (1ull << 29)) break;
+  }
+  if (shift > 12) return 0;
+  const uint64_t bytes = units << shift;
+  size_t fr = 0, tot = 0;
+  HIP_OK(hipMemGetInfo(&fr, &tot));
+  if (bytes > fr / 10 * 7) return 0;  // leave room for the search scratch
+  std::vector<uint32_t> kw(n, 0u);
+  uint64_t u = 0;
+  for (uint64_t v = 1; v < n; v++) {
+    kw[v] = (uint32_t)(u << 3) | (uint32_t)(nb[v] - 1);
+    u += (nb[v] * rec_per_block + (1ull << shift) - 1) >> shift;
+  }
+  HIP_OK(q.qkw.upload(kw.data(), n));
+  HIP_OK(q.recs.alloc(bytes));
+  HIP_OK(launch_qg_pack(q.qids.p, q.id_stride, q.qcodes.p, q.code_stride, q.Me, (uint32_t)n, q.qkw.p, shift, q.recs.p,
+                        ix->stream));
+  HIP_OK(hipStreamSynchronize(ix->stream));
+  q.rec_shift = shift;
+  q.rec_bytes = bytes;
+  q.packed = true;
+  return 0;
+}
+
+extern "C" uint64_t ngt_amd_qg_record_bytes(const ngt_amd_index* ix) {
+  return ix && ix->qg.has_graph && ix->qg.packed ? ix->qg.rec_bytes : 0;
+}
+
 static int alloc_qg_graph(ngt_amd_index* ix, uint64_t maxdeg) {
   QgState& q = ix->qg;
   const uint32_t stride = (uint32_t)std::max<uint64_t>(16, (maxdeg + 15) & ~15ull);
@@ -151,7 +211,7 @@ extern "C" int ngt_amd_qg_build_graph(ngt_amd_index* ix, const uint8_t* local_co
   HIP_OK(launch_qg_build(a, ix->stream));
   HIP_OK(hipStreamSynchronize(ix->stream));
   q.has_graph = true;
-  return 0;
+  return qg_pack(ix);
 }
 
 extern "C" int ngt_amd_qg_set_graph(ngt_amd_index* ix, const uint64_t* qoff, const uint32_t* qids,
@@ -183,7 +243,7 @@ extern "C" int ngt_amd_qg_set_graph(ngt_amd_index* ix, const uint64_t* qoff, con
   HIP_OK(hipMemcpy(q.qids.p, hid.data(), hid.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(q.qcodes.p, hcode.data(), hcode.size(), hipMemcpyHostToDevice));
   q.has_graph = true;
-  return 0;
+  return qg_pack(ix);
 }
 
 extern "C" uint32_t ngt_amd_qg_max_degree(const ngt_amd_index* ix) {
@@ -326,6 +386,9 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   a.qcodes = q.qcodes.p;
   a.code_stride = q.code_stride;
   a.Me = q.Me;
+  a.recs = q.packed ? q.recs.p : nullptr;
+  a.qkw = q.qkw.p;
+  a.rec_shift = q.rec_shift;
   a.queries = static_cast<const uint8_t*>(d_queries);
   a.query_bytes = query_bytes;
   a.nq = nq;

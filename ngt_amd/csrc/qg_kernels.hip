@@ -129,6 +129,61 @@ __global__ void __launch_bounds__(256) ngt_qg_build_kernel(QgBuildArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Packed search layout.  The fixed-stride slabs give every node id_stride/16
+// code blocks, and an expansion loads them all before it knows the degree
+// (on a 128-slot ANNG-based graph with ~42 neighbours, 5 of 8 KiB per
+// expansion for nothing).  The packed layout keeps the reference's per-node
+// ceil(deg/16) blocks (QuantizedGraphRepository, QuantizedGraph.h:74-113):
+// node v's record -- its code blocks, then 16 entries {neighbour id,
+// neighbour key word} per block -- sits at unit u(v) of a byte array, records
+// in id order; kw(v) = u(v) << 3 | (blocks(v) - 1).  The search's unchecked
+// keys carry kw in place of the id (u(v) grows strictly with v, so
+// (distance, kw) orders exactly as (distance, id)), so a pop knows where the
+// record is and how long, and issues exactly its loads in one round trip.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) ngt_qg_blocks_kernel(const uint32_t* qids, uint32_t id_stride,
+                                                            uint32_t nrows, uint8_t* nb) {
+  const uint32_t warps = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  for (uint32_t v = w0; v < nrows; v += warps) {
+    const uint32_t* ids = qids + (uint64_t)v * id_stride;
+    uint32_t deg = 0;
+    for (uint32_t j = 0; j < id_stride; j += 64)
+      deg += (uint32_t)__popcll(ballot64(j + lane < id_stride && ids[j + lane] != 0u));
+    // a node without edges keeps one empty block: every record is at least
+    // one unit, so the key words stay strictly increasing with the id
+    if (lane == 0) nb[v] = (uint8_t)(deg == 0 ? 1u : (deg - 1) / 16 + 1);
+  }
+}
+
+__global__ void __launch_bounds__(256) ngt_qg_pack_kernel(const uint32_t* qids, uint32_t id_stride,
+                                                          const uint8_t* qcodes, uint64_t code_stride, uint32_t Me,
+                                                          uint32_t nrows, const uint32_t* qkw, uint32_t rec_shift,
+                                                          uint8_t* recs) {
+  const uint32_t warps = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const uint64_t blk = (uint64_t)8 * Me;
+  for (uint32_t v = 1 + w0; v < nrows; v += warps) {
+    const uint32_t kw = qkw[v];
+    const uint32_t nb = (kw & 7u) + 1u;
+    uint8_t* rec = recs + ((uint64_t)(kw >> 3) << rec_shift);
+    const uint4* src = reinterpret_cast<const uint4*>(qcodes + (uint64_t)v * code_stride);
+    uint4* dst = reinterpret_cast<uint4*>(rec);
+    const uint64_t n16 = nb * blk / 16;
+    const uint64_t have = code_stride / 16;
+    for (uint64_t t = lane; t < n16; t += 64) dst[t] = t < have ? src[t] : make_uint4(0, 0, 0, 0);
+    uint2* ent = reinterpret_cast<uint2*>(rec + nb * blk);
+    const uint32_t* ids = qids + (uint64_t)v * id_stride;
+    for (uint32_t i = lane; i < 16 * nb; i += 64) {
+      const uint32_t id = i < id_stride ? ids[i] : 0u;
+      ent[i] = make_uint2(id, id ? qkw[id] : 0u);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Encoder (the local half of Quantizer::insert, lib/NGT/NGTQ/Quantizer.h:
 // 1895-1959): residual subvector r = object - global centroid, computed in
 // double and stored as float (GenerateResidualObjectFloat, :1407-1435), coded
@@ -647,6 +702,98 @@ __device__ __forceinline__ uint32_t ids_and_adc(const LaneLut<PPL>& L, const uin
   return deg;
 }
 
+// ids_and_adc over a packed record (the node's key word gave `rec` and its
+// `nb` <= NB blocks): exactly the node's code blocks and 16*nb entries load
+// together; nid / nkw receive the neighbour ids and key words.
+template <int PPL, int NB>
+__device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, const uint8_t* rec, uint32_t nb,
+                                                       uint32_t Me, float scale, float toff, uint32_t* nid,
+                                                       uint32_t* nkw, float* dists, bool probe, const SearchState& st,
+                                                       const uint8_t* vis, uint32_t epoch, uint64_t (&seen)[2]) {
+  const int lane = lane_id();
+  const uint32_t npairs = Me >> 1;
+  const uint64_t blk = (uint64_t)8 * Me;
+  const qg_i32x4 onehot = qg_onehot_b();
+  (void)onehot;
+  uint4 c[NB][PPL];
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+#pragma unroll
+    for (int s = 0; s < PPL; s++) {
+      const uint32_t p = (uint32_t)lane + 64u * s;
+      c[j][s] = make_uint4(0, 0, 0, 0);
+      if ((uint32_t)j < nb && p < npairs)
+        c[j][s] = *reinterpret_cast<const uint4*>(rec + (uint64_t)j * blk + (uint64_t)p * 16);
+    }
+  }
+  static_assert(NB <= 8, "two 64-id chunks at most");
+  constexpr int NC = (16 * NB + 63) / 64;
+  const uint2* ent = reinterpret_cast<const uint2*>(rec + (uint64_t)nb * blk);
+  const uint32_t ne = 16 * nb;
+  uint32_t deg = 0;
+  uint32_t idr[NC];
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) {
+    const uint32_t j = 64u * cc;
+    const uint2 e = j + lane < ne ? ent[j + lane] : make_uint2(0u, 0u);
+    idr[cc] = e.x;
+    if (j < ne) {
+      nid[j + lane] = e.x;
+      nkw[j + lane] = e.y;
+    }
+    deg += (uint32_t)__popcll(ballot64(e.x != 0u));
+  }
+  bool pre[NC];
+  uint32_t word[NC];
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) {
+    pre[cc] = false;
+    word[cc] = 0;
+    if (probe && idr[cc] != 0u) {
+      const uint32_t b = (idr[cc] * 0x85EBCA77u) >> st.vf_shift;
+      pre[cc] = (st.vf[b >> 5] >> (b & 31)) & 1u;
+      if (pre[cc])
+        word[cc] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (idr[cc] & ~3u)), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  const uint32_t nbd = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+#if NGT_AMD_QG_VALU_REDUCE
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    if ((uint32_t)j < nbd) {
+      uint32_t v[16];
+      block_partials<PPL>(L, c[j], v);
+      const uint32_t r = reduce_scatter16(v);
+      const uint32_t o = (uint32_t)j * 16 + qg_obj_of_lane(lane);
+      if ((lane & 3) == 0 && o < deg) dists[o] = adc_epilogue(r, scale, toff);
+    }
+  }
+#else
+  const uint32_t base = 0x03020100u;
+#pragma unroll
+  for (int q = 0; q < (NB + 3) / 4; q++) {
+    if ((uint32_t)(4 * q) < nbd) {
+      uint32_t part[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int j = 4 * q + u;
+        part[u] = 0;
+        if (j < NB && (uint32_t)j < nbd) part[u] = adc_part_mfma<PPL>(L, c[j < NB ? j : 0], onehot, base);
+      }
+      const uint32_t r = fold4(part[0], part[1], part[2], part[3]);
+      const uint32_t o = (uint32_t)(4 * q) * 16 + (uint32_t)lane;
+      if (o < deg) dists[o] = adc_epilogue_total(r, Me, scale, toff);
+    }
+  }
+#endif
+  seen[0] = seen[1] = 0;
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++)
+    seen[cc] = ballot64(pre[cc] && ((word[cc] >> (8 * (idr[cc] & 3))) & 0xffu) == epoch);
+  return deg;
+}
+
 // Standalone ADC: wave per (query, node) pair; out[i*out_stride + j] for the
 // node's neighbours j (full list, the QG loop's call at QuantizedGraph.h:240).
 template <int PPL>
@@ -752,7 +899,10 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
   p += (size_t)4 * nstage64;
   st.nd = reinterpret_cast<float*>(p);
   p += (size_t)4 * nstage64;
+  uint32_t* nkw = reinterpret_cast<uint32_t*>(p);  // packed layout: the neighbours' key words
+  p += (size_t)4 * nstage64;
   float* qlds = reinterpret_cast<float*>(p);
+  const bool packed = a.recs != nullptr;
 
   const uint32_t slot = blockIdx.x;
   uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
@@ -808,7 +958,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       if ((uint32_t)lane < m) {
         const uint32_t id = st.nid[lane];
         visit(a.ht_log2, st, id, bitmap_mode, vis, epoch);
-        const uint64_t key = make_key(st.nd[lane], id);
+        const uint64_t key = make_key(st.nd[lane], packed ? a.qkw[id] : id);
         if (ncq + lane < a.cq_cap) st.cq[ncq + lane] = key;
         else spill[nspill + (ncq + lane - a.cq_cap)] = key;
       }
@@ -894,13 +1044,20 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       NGT_MARK(t_pop);
 
       // neighbour ids (0-terminated fixed-stride row) and their ADC distances
-      const uint32_t target = key_id(wbest);
+      const uint32_t target = key_id(wbest);  // the node id, or its key word in the packed layout
       const uint32_t* nbr = a.qids + (uint64_t)target * a.id_stride;
       uint32_t deg = 0;
       uint64_t seen_pre[2] = {0, 0};
       const bool early = NB > 0 && a.id_stride <= 16u * NB;
       const bool probe = early && !use_hash && st.vf != nullptr;
-      if (early) {
+      if (packed) {
+        // the key word names the record and its block count (qg_api.cpp qg_pack)
+        const uint8_t* rec = a.recs + ((uint64_t)(target >> 3) << a.rec_shift);
+        deg = ids_and_adc_packed<PPL, (NB > 0 ? NB : 1)>(L, rec, (target & 7u) + 1u, a.Me, scale, toff, st.nid, nkw,
+                                                         st.nd, !use_hash && st.vf != nullptr, st, vis, epoch,
+                                                         seen_pre);
+        NGT_MARK(t_ids);
+      } else if (early) {
         deg = ids_and_adc<PPL, (NB > 0 ? NB : 1)>(L, nbr, a.id_stride, a.qcodes + (uint64_t)target * a.code_stride,
                                                   a.Me, scale, toff, st.nid, st.nd, probe, st, vis, epoch, seen_pre);
         NGT_MARK(t_ids);
@@ -924,8 +1081,9 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       for (uint32_t base = 0; base < deg; base += 64) {
         const uint32_t i = base + lane;
         const bool in = i < deg && st.nd[i] <= expr;
-        const bool seen = in && (probe ? ((((base == 0) ? seen_pre[0] : seen_pre[1]) >> lane) & 1ull) != 0
-                                       : visited_test(a.ht_log2, st, st.nid[i], bitmap_mode, vis, epoch));
+        const bool pre_probed = packed ? (!use_hash && st.vf != nullptr) : probe;
+        const bool seen = in && (pre_probed ? ((((base == 0) ? seen_pre[0] : seen_pre[1]) >> lane) & 1ull) != 0
+                                            : visited_test(a.ht_log2, st, st.nid[i], bitmap_mode, vis, epoch));
         uint64_t cand = ballot64(in && !seen);
         uint64_t acc = 0;
         while (cand) {
@@ -934,7 +1092,10 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
           const float d = st.nd[base + j];
           if (!(d <= expr)) continue;
           acc |= 1ull << j;
-          const uint64_t key = make_key(d, st.nid[base + j]);
+          // results by (distance, id); the unchecked set by (distance, key
+          // word) in the packed layout -- the same order
+          const uint64_t rkey = make_key(d, st.nid[base + j]);
+          const uint64_t key = packed ? make_key(d, nkw[base + j]) : rkey;
           // keys beyond expr can never be popped; expr only shrinks, so a
           // compaction at an unchanged expr would drop nothing
           if (ncq >= a.cq_cap && expr != cq_cut) {
@@ -962,7 +1123,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
             }
           }
           if (d <= radius) {
-            res_insert(st.res, nres, size, key);
+            res_insert(st.res, nres, size, rkey);
             if (nres >= size) {
               radius = key_dist(st.res[size - 1]);
               expr = __fmul_rn(a.coef, radius);
@@ -1106,9 +1267,28 @@ size_t qg_search_lds_bytes(const QgSearchArgs& a) {
   b += a.vf_log2 ? ((size_t)1 << a.vf_log2) / 8 : 0;
   b += 2 * (((size_t)8 * (a.size + 1) + 15) & ~(size_t)15);
   const uint32_t nstage = a.id_stride > a.size ? a.id_stride : a.size;
-  b += (size_t)8 * ((nstage + 63) & ~63u);
+  b += (size_t)12 * ((nstage + 63) & ~63u);
   b += (size_t)a.dp * 4;
   return b;
+}
+
+hipError_t launch_qg_blocks(const uint32_t* qids, uint32_t id_stride, uint32_t nrows, uint8_t* nb, hipStream_t s) {
+  if (nrows == 0) return hipSuccess;
+  uint64_t blocks = ((uint64_t)nrows + 3) / 4;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(ngt_qg_blocks_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, qids, id_stride, nrows, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_qg_pack(const uint32_t* qids, uint32_t id_stride, const uint8_t* qcodes, uint64_t code_stride,
+                          uint32_t Me, uint32_t nrows, const uint32_t* qkw, uint32_t rec_shift, uint8_t* recs,
+                          hipStream_t s) {
+  if (nrows < 2) return hipSuccess;
+  uint64_t blocks = ((uint64_t)nrows + 3) / 4;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(ngt_qg_pack_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, qids, id_stride, qcodes,
+                     code_stride, Me, nrows, qkw, rec_shift, recs);
+  return hipGetLastError();
 }
 
 hipError_t launch_qg_search(const QgSearchArgs& a, uint32_t slots, hipStream_t s) {

@@ -293,8 +293,13 @@ def qg_search_batch(qg, rows, queries, seeds, k, epsilon, expansion, luts, scale
     rows = np.ascontiguousarray(rows, dtype=np.float32)
     queries = np.ascontiguousarray(queries, dtype=np.float32)
     nq = queries.shape[0]
-    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
-    so = np.arange(nq + 1, dtype=np.uint64) * np.uint64(seeds.shape[1])
+    if isinstance(seeds, np.ndarray) and seeds.ndim == 2:
+        so = np.arange(nq + 1, dtype=np.uint64) * np.uint64(seeds.shape[1])
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32).reshape(-1)
+    else:  # ragged lists (tree seeds)
+        so = np.zeros(nq + 1, np.uint64)
+        so[1:] = np.cumsum([len(s) for s in seeds])
+        seeds = np.ascontiguousarray(np.concatenate([np.asarray(s, np.uint32) for s in seeds]), dtype=np.uint32)
     stride = max(k, int(k * expansion) + 1)
     ids = np.zeros((nq, stride), np.uint32)
     ds = np.zeros((nq, stride), np.float32)

@@ -351,22 +351,27 @@ def test_ngtqg_quantize_capi(tmp_path):
     qi.close()
 
 
-def _synthetic_qg(dim, n, maxe, seed):
+def _synthetic_qg(dim, n, maxe, seed, dups=(), degrees=None):
     """A QG index over n random rows of `dim` floats (dsub 1 => M = dim): a
     kNN graph, random codebooks and nearest-centroid codes, in both the
-    oracle's form (read_qg's dict) and the device's."""
+    oracle's form (read_qg's dict) and the device's.  dups: (dst, src) rows
+    copied (equal codes, so equal ADC distances); degrees: per-node list
+    lengths (0 = a node without edges), default maxe everywhere."""
     rng = np.random.default_rng(seed)
     dp = F.padded_dim(dim)
     rows = np.zeros((n + 1, dp), np.float32)
     rows[1:, :dim] = rng.random((n, dim), dtype=np.float32)
+    for dst, src in dups:
+        rows[dst] = rows[src]
     x = rows[1:, :dim].astype(np.float64)
     sq = (x * x).sum(1)
     d2 = sq[:, None] + sq[None, :] - 2.0 * x @ x.T
     np.fill_diagonal(d2, np.inf)
     nn = np.argsort(d2, axis=1, kind="stable")[:, :maxe] + 1
+    deg = np.full(n, maxe, np.int64) if degrees is None else np.asarray(degrees, np.int64)
     offs = np.zeros(n + 2, np.uint64)
-    offs[2:] = np.cumsum(np.full(n, maxe, np.uint64))
-    ids = nn.reshape(-1).astype(np.uint32)
+    offs[2:] = np.cumsum(deg.astype(np.uint64))
+    ids = np.concatenate([nn[i, :deg[i]] for i in range(n)]).astype(np.uint32)
     M = dim
     local = np.zeros((M, 17, 1), np.float32)
     local[:, 1:, 0] = rng.random((M, 16), dtype=np.float32)
@@ -446,4 +451,58 @@ def test_qg_train_local_ngt_equals_reference_codebooks():
     local = ix.qg_train_ngt(rows, dsub=1)
     st = np.load(os.path.join(GOLD, "qg_kmeans_st.npz"))["c1"]
     assert np.array_equal(local[:, :, 0].view(np.uint32), st.view(np.uint32))
+    ix.close()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_qg_packed_layout_equals_fixed(monkeypatch, name):
+    """The packed search layout (per node ceil(deg/16) blocks + {id, key word}
+    entries, keys carrying the key word; qg_api.cpp qg_pack) and the fixed
+    slabs give the same ids, distance bits and work counters, including the
+    code-block count; the records take sum(ceil(deg/16) * (8*Me + 128)) bytes
+    rounded to their unit."""
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state(name)
+    ix = device_qg(name)
+    rec = int(ix.L.ngt_amd_qg_record_bytes(ix.h))
+    assert rec > 0
+    deg = np.diff(qg["qoff"].astype(np.int64))[1:rows.shape[0]]
+    nb = np.maximum(1, (deg + 15) // 16)
+    me = (qg["M"] + 1) // 2 * 2
+    per = nb * (8 * me + 128)
+    assert rec >= int(per.sum()) and rec <= int(per.sum()) + 4096 * len(per)
+    monkeypatch.setenv("NGT_AMD_QG_PACKED", "0")
+    fx = device_qg(name)
+    assert int(fx.L.ngt_amd_qg_record_bytes(fx.h)) == 0
+    qs = z["queries"].astype(np.float32)
+    for k, eps, exp in [(10, 0.05, 3.0), (20, 0.2, 2.0), (10, 0.1, 0.5)]:
+        for vis in (-1, 0):
+            a = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_TREE, visited_hash_log2=vis)
+            b = fx.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_TREE, visited_hash_log2=vis)
+            assert np.array_equal(a[2], b[2])
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
+            assert np.array_equal(a[3][:, :5], b[3][:, :5])
+    ix.close()
+    fx.close()
+
+
+def test_qg_packed_layout_ties_and_isolated_nodes():
+    """Duplicate rows (equal ADC distances, ordered by id) and nodes without
+    edges (one empty block each) through the packed layout: the oracle's ids,
+    distance bits and counters."""
+    n = 900
+    degrees = [(7 * i) % 41 for i in range(n)]  # 0..40 edges, some nodes none
+    qg, rows, ix = _synthetic_qg(128, n, 40, 77, dups=[(6, 5), (7, 5), (300, 299)], degrees=degrees)
+    assert int(ix.L.ngt_amd_qg_record_bytes(ix.h)) > 0
+    rng = np.random.default_rng(9)
+    qs = rng.random((8, 128), dtype=np.float32)
+    qs[0] = rows[5, :128]
+    seeds = [np.array([1 + 91 * i, 450 + i, 5], np.uint32) for i in range(len(qs))]
+    for k, eps, exp in [(10, 0.1, 3.0), (20, 0.3, 2.0)]:
+        gi, gd, gn, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_GIVEN,
+                                       seeds=seeds)
+        for qi, q in enumerate(qs):
+            oid, od, ocnt = O.qg_search(qg, rows, q, seeds[qi], k, np.float32(eps), np.float32(exp))
+            assert list(gi[qi, :gn[qi]]) == list(oid), (k, qi)
+            assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32)), (k, qi)
+            assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt], (k, qi)
     ix.close()
