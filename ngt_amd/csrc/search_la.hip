@@ -1032,23 +1032,13 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
     }                                                                                                           \
     hipLaunchKernelGGL(kern, dim3(slots), dim3(64 * W), lds, s, a);                                             \
   } while (0)
-#define LA_T(NCH, PW)                                                                                           \
-  do {                                                                                                          \
-    if (la_wpe() == 4) {                                                                                        \
-      if (full) LA(NCH, 1, PW, 3, 1, true, 4); else LA(NCH, 1, PW, 3, 1, false, 4);                             \
-    } else {                                                                                                    \
-      if (full) LA(NCH, 1, PW, 6, 1, true, 3); else LA(NCH, 1, PW, 6, 1, false, 3);                             \
-    }                                                                                                           \
-  } while (0)
   if (mode == 0) {
-    if (P == 3) {
-      if (a.dp == 128) LA_T(8, 3); else LA_T(6, 3);
-    } else if (P == 2) {
-      if (a.dp == 128) LA_T(8, 2); else LA_T(6, 2);
-    } else if (P == 1) {
-      if (a.dp == 128) LA_T(8, 1); else LA_T(6, 1);
+    // P = 2 targets per step, 4 resident waves per SIMD (ngt_kernels.h)
+    if (P != 2 || la_wpe() != 4) return hipErrorNotSupported;
+    if (a.dp == 128) {
+      if (full) LA(8, 1, 2, 3, 1, true, 4); else LA(8, 1, 2, 3, 1, false, 4);
     } else {
-      if (a.dp == 128) LA_T(8, 4); else LA_T(6, 4);
+      if (full) LA(6, 1, 2, 3, 1, true, 4); else LA(6, 1, 2, 3, 1, false, 4);
     }
   } else {
     // latency form: one workgroup per CU, 2 waves per SIMD -> room for 192
@@ -1059,7 +1049,6 @@ hipError_t launch_graph_search_la(const SearchArgs& a, int mode, bool full, uint
       if (full) LA(6, 8, 1, 12, 1, true, 2); else LA(6, 8, 1, 12, 1, false, 2);
     }
   }
-#undef LA_T
 #undef LA
   return hipGetLastError();
 }
