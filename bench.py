@@ -445,12 +445,14 @@ def main():
     tree = None
     anng_check = None
     capi_dir = None
+    capi_tmp = False
     if (args.graph == "anng" and world == 1 and not args.pmc_launches and N == 1_000_000 and D == 128
             and args.anng_batch == 200 and (args.capi_line == "on" or args.capi_line == "auto")):
         # the C-API line opens the index this run saves (ngt_save_index) from disk
         import tempfile
         if not args.anng_dir:
             capi_dir = args.anng_dir = tempfile.mkdtemp(prefix="ngt_anng_capi_")
+            capi_tmp = True
         else:
             capi_dir = args.anng_dir
     if args.graph == "anng":
@@ -822,7 +824,7 @@ def main():
     capi = None
     if rank == 0 and capi_dir:
         capi = capi_anng_line(capi_dir, qry, gt, D, K, chosen, args.threads)
-        if not (args.anng_dir and args.anng_dir != capi_dir):
+        if capi_tmp:
             import shutil
             shutil.rmtree(capi_dir, ignore_errors=True)
 

@@ -319,10 +319,10 @@ std::string ngt_amd::device_error_text(int flag) {
       "one-expansion kernel: stale chunk minimum (invariant)",                // 4: search_kernels.hip
       "lookahead kernel: selection target exceeded by equal keys (invariant)",  // 8: search_la.hip
       "latency kernel: a speculation slot never became ready (timeout)",      // 16: search_lat.hip
-      "latency kernel: tail-to-spill threshold selection check",              // 32
-      "latency kernel: spill refill selection check",                         // 64
-      "latency kernel: head refill selection check",                          // 128
-      "NGTQG kernel: spill chunk minimum not found (invariant)",               // 256: qg_kernels.hip
+      "latency / NGTQG kernel: tail-to-spill threshold selection check",      // 32
+      "latency / NGTQG kernel: spill refill selection check",                 // 64
+      "latency / NGTQG kernel: head refill selection check",                  // 128
+      "(unused since round 5)",                                               // 256
   };
   std::string out;
   for (int b = 0; b < 31; b++) {
@@ -705,6 +705,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       SearchArgs b = a;
       b.lat_slots = cap <= 64 ? 32u : 16u;
       b.lat_tail = 4096u;
+      b.lat_hop = lat_hop_default();
       while (search_lat_lds_bytes(b) > lds_max && b.lat_tail > 512u) b.lat_tail -= 256u;
       while (search_lat_lds_bytes(b) > lds_max && b.lat_slots > 8u) b.lat_slots -= 2u;
       // test knobs: a small tail forces the HBM spill, few slots the orphan path

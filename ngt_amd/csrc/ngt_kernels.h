@@ -97,6 +97,7 @@ struct SearchArgs {
   // latency kernel (search_lat.hip): speculation slots and LDS tail keys
   uint32_t lat_slots;
   uint32_t lat_tail;
+  uint32_t lat_hop;              // latency kernel: warm L2 for the nearest fresh neighbour of each list part
   // launch schedule (ngt_amd_api.cpp run_search, "probe and resume"): the
   // w-th work item a slot claims is query order[w] (null: w), and a launch
   // has *nwork_dev work items (null: nq).  A probe launch (pause_after > 0)
@@ -203,6 +204,15 @@ inline uint32_t la_targets(int mode) {
 // workgroups fit a CU; ANNG 72.0k QPS) or 3 (168 VGPRs, 6 groups, 512 keys,
 // 32 Kbit; 64.7k QPS): 4
 inline int la_wpe() { return 4; }
+// latency kernel: hop prefetch of each list part's nearest fresh neighbour
+// (search_lat.hip); NGT_AMD_LAT_HOP=0 turns it off (A/B)
+inline uint32_t lat_hop_default() {
+  static const uint32_t v = [] {
+    const char* e = ngt_amd::knob("NGT_AMD_LAT_HOP");
+    return e ? (atoi(e) != 0 ? 1u : 0u) : 1u;
+  }();
+  return v;
+}
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 uint32_t search_lat_lds_bytes(const SearchArgs& a);
 hipError_t launch_graph_search_lat(const SearchArgs& a, uint32_t slots, hipStream_t s);

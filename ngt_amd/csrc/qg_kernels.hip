@@ -856,22 +856,6 @@ __device__ __forceinline__ void qg_exact(const float* qlds, const QgSearchArgs& 
   }
 }
 
-// Minimum of spill chunk c (keys c*64 .. min(n, c*64+64)), wave-uniform.
-__device__ __forceinline__ uint64_t chunk_min(const uint64_t* spill, uint32_t c, uint32_t n) {
-  const uint32_t i = c * 64 + lane_id();
-  return wave_min_u64(i < n ? spill[i] : ~0ull);
-}
-
-// Every chunk minimum of an n-key spill (after a compaction or the seeds);
-// tmin <- the last chunk's.
-__device__ __forceinline__ void spill_rebuild(const uint64_t* spill, uint64_t* cmin, uint32_t n, uint64_t& tmin) {
-  tmin = ~0ull;
-  for (uint32_t c = 0; c < ((n + 63) >> 6); c++) {
-    tmin = chunk_min(spill, c, n);
-    if (lane_id() == 0) cmin[c] = tmin;
-  }
-}
-
 // NB > 0: id rows of up to 16*NB entries load together with all their code
 // blocks (ids_and_adc); NB = 0: ids, then the codes of the degree read.
 template <int PPL, int NCH, int NB>
@@ -901,16 +885,14 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
   p += (size_t)4 * nstage64;
   uint32_t* nkw = reinterpret_cast<uint32_t*>(p);  // packed layout: the neighbours' key words
   p += (size_t)4 * nstage64;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(p);  // threshold selection: 64 counters, then 64 staged keys
+  p += 256 + 512;
   float* qlds = reinterpret_cast<float*>(p);
   const bool packed = a.recs != nullptr;
 
   const uint32_t slot = blockIdx.x;
   uint8_t* vis = a.vis + (uint64_t)slot * a.vis_stride;
-  // HBM spill of the unchecked set in chunks of 64 keys, each chunk's exact
-  // minimum after the key area: a pop reads the chunk minima, not every key
-  uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;
-  const uint32_t scap = (uint32_t)(((uint64_t)a.spill_cap * 64 / 65) & ~(uint64_t)63);
-  uint64_t* cmin = spill + scap;
+  uint64_t* spill = a.spill + (uint64_t)slot * a.spill_cap;  // the unchecked set's HBM level
   const uint32_t hcap = use_hash ? 1u << a.ht_log2 : 0u;
   const uint32_t hlimit = hcap - (hcap >> 2);
   const uint32_t npairs = a.Me >> 1;
@@ -937,14 +919,194 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
     if (lane == 0) a.slot_epoch[slot] = epoch;
 
     bool bitmap_mode = !use_hash;
-    uint32_t nvisited = 0, ncq = 0, nspill = 0, nres = 0, maxq = 0;
-    uint64_t tmin = ~0ull;                   // minimum of the last spill chunk
-    float cq_cut = -1.0f, sp_cut = -1.0f;   // expr of the last compactions
+    uint32_t nvisited = 0, nres = 0, maxq = 0;
     uint64_t nadc = 0, nacc = 0, nexp = 0, nexact = 0, nblk = 0;
     uint64_t t_pop = 0, t_ids = 0, t_adc = 0, t_acc = 0, t_last = 0;
     (void)t_pop; (void)t_ids; (void)t_adc; (void)t_acc; (void)t_last;
     const uint32_t size = a.size;
     float radius = a.radius;
+    float expr = __fmul_rn(a.coef, radius);
+
+    // ---- the unchecked set: a sorted head of the 64 smallest keys in
+    // registers (lane i = i-th smallest, hn keys) < B <= an unsorted LDS tail
+    // (st.cq, ntail keys) < T <= an HBM spill (nspill keys) -- the latency
+    // kernel's form (search_lat.hip), so a pop is a lane shift and never scans
+    // anything: a quantized graph over 12.5M objects keeps ~40k unchecked keys
+    // per query, and the chunk-minimum scans of a flat spill were most of its
+    // expansions' time.  Exact throughout; keys beyond the exploration radius
+    // are dropped when the tail fills (they can never be popped,
+    // QuantizedGraph.h:226-229 / Graph.cpp:433-435).
+    uint64_t hk = ~0ull, B = ~0ull, T = ~0ull;
+    uint32_t hn = 0, ntail = 0, nspill = 0;
+    uint64_t* tail = st.cq;
+    auto spill_push = [&](uint64_t key) {
+      if (nspill >= a.spill_cap) {
+        if (lane == 0) atomicOr(a.error, 1);
+      } else {
+        if (lane == 0) spill[nspill] = key;
+        nspill++;
+      }
+    };
+    auto tail_room = [&]() {
+      uint32_t out = 0;
+      for (uint32_t b0 = 0; b0 < ntail; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < ntail ? tail[i] : ~0ull;
+        const bool keep = i < ntail && key_dist(key) <= expr;
+        const uint64_t km = ballot64(keep);
+        __builtin_amdgcn_wave_barrier();
+        if (keep) tail[out + mbcnt(km)] = key;
+        __builtin_amdgcn_wave_barrier();
+        out += (uint32_t)__popcll(km);
+      }
+      ntail = out;
+      const uint32_t keep = a.cq_cap / 2;
+      if (ntail <= keep) return;
+      const uint64_t l = lat_select(tail, ntail, keep, ~0ull, hist);
+      out = 0;
+      for (uint32_t b0 = 0; b0 < ntail; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < ntail ? tail[i] : ~0ull;
+        const bool mv = i < ntail && key >= l;
+        const bool kp = i < ntail && key < l;
+        const uint64_t mm = ballot64(mv), km = ballot64(kp);
+        const uint32_t nm = (uint32_t)__popcll(mm);
+        if (nspill + nm > a.spill_cap) {
+          if (lane == 0) atomicOr(a.error, 1);
+        } else if (mv) {
+          spill[nspill + mbcnt(mm)] = key;
+        }
+        if (nspill + nm <= a.spill_cap) nspill += nm;
+        __builtin_amdgcn_wave_barrier();
+        if (kp) tail[out + mbcnt(km)] = key;
+        __builtin_amdgcn_wave_barrier();
+        out += (uint32_t)__popcll(km);
+      }
+      if ((out == 0u || out > keep) && lane == 0) atomicOr(a.error, 32);  // selection check
+      ntail = out;
+      T = l;
+    };
+    auto tail_push = [&](uint64_t key) {
+      if (key >= T) {
+        spill_push(key);
+      } else {
+        if (ntail >= a.cq_cap) tail_room();
+        if (key >= T) {
+          spill_push(key);
+        } else {
+          if (lane == 0) tail[ntail] = key;
+          ntail++;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    };
+    auto insert_key = [&](uint64_t key) {
+      if (key < B) {
+        const uint32_t pos = (uint32_t)__popcll(ballot64((uint32_t)lane < hn && hk < key));
+        if (hn == 64u) {
+          // the head is full: its largest key (or this one) moves to the tail
+          if (pos == 64u) {
+            B = key;
+            tail_push(key);
+          } else {
+            const uint64_t e = readlane_u64(hk, 63);
+            const uint64_t uk = wave_up1_u64(hk);
+            if ((uint32_t)lane > pos) hk = uk;
+            if ((uint32_t)lane == pos) hk = key;
+            B = e;
+            tail_push(e);
+          }
+        } else {
+          const uint64_t uk = wave_up1_u64(hk);
+          if ((uint32_t)lane > pos && (uint32_t)lane <= hn) hk = uk;
+          if ((uint32_t)lane == pos) hk = key;
+          hn++;
+        }
+      } else {
+        tail_push(key);
+      }
+      const uint32_t q = hn + ntail + nspill;
+      if (q > maxq) maxq = q;
+    };
+    // an empty tail takes the smallest spill keys within the radius (the ones
+    // beyond it are dropped)
+    auto refill_tail = [&]() {
+      const uint32_t want = a.cq_cap / 2;
+      const uint64_t lim = ((uint64_t)ord_of(expr) << 32) | 0xffffffffull;
+      const uint64_t l = lat_select(spill, nspill, want, lim, hist);
+      if (l == 0ull) {  // nothing within the radius: the search ends
+        nspill = 0;
+        T = ~0ull;
+        return;
+      }
+      uint32_t out = 0;
+      for (uint32_t b0 = 0; b0 < nspill; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < nspill ? spill[i] : ~0ull;
+        const bool in = i < nspill && key <= lim;
+        const bool mv = in && key < l;
+        const bool sy = in && !mv;
+        const uint64_t mm = ballot64(mv), sm = ballot64(sy);
+        __builtin_amdgcn_wave_barrier();
+        if (mv) tail[ntail + mbcnt(mm)] = key;
+        if (sy) spill[out + mbcnt(sm)] = key;
+        __builtin_amdgcn_wave_barrier();
+        ntail += (uint32_t)__popcll(mm);
+        out += (uint32_t)__popcll(sm);
+      }
+      nspill = out;
+      T = nspill ? l : ~0ull;
+      if ((ntail == 0u || ntail > want) && lane == 0) atomicOr(a.error, 64);  // selection check
+    };
+    // an empty head takes the (at most 64) smallest tail keys, sorted across
+    // the lanes by a bitonic network
+    auto refill_head = [&]() {
+      if (ntail == 0 && nspill != 0) refill_tail();
+      if (ntail == 0) return;
+      const uint64_t t = lat_select(tail, ntail, 64u, ~0ull, hist);
+      uint64_t* st64 = reinterpret_cast<uint64_t*>(hist + 64);  // 64 staged keys
+      uint32_t got = 0, out = 0;
+      for (uint32_t b0 = 0; b0 < ntail; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < ntail ? tail[i] : ~0ull;
+        const bool mv = i < ntail && key < t;
+        const bool kp = i < ntail && !mv;
+        const uint64_t mm = ballot64(mv), km = ballot64(kp);
+        __builtin_amdgcn_wave_barrier();
+        if (mv) st64[got + mbcnt(mm)] = key;
+        if (kp) tail[out + mbcnt(km)] = key;
+        __builtin_amdgcn_wave_barrier();
+        got += (uint32_t)__popcll(mm);
+        out += (uint32_t)__popcll(km);
+      }
+      uint64_t v = (uint32_t)lane < got ? st64[lane] : ~0ull;
+      ntail = out;
+      if ((got == 0u || got > 64u) && lane == 0) atomicOr(a.error, 128);  // selection check
+#pragma unroll
+      for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+          const uint64_t o = shfl_xor_u64(v, j);
+          const bool up = ((lane & kk) == 0);
+          const bool lower = (lane & j) == 0;
+          const uint64_t mn = o < v ? o : v, mx = o < v ? v : o;
+          v = (lower == up) ? mn : mx;
+        }
+      }
+      hk = v;
+      hn = got;
+      B = (ntail + nspill) ? readlane_u64(hk, (int)got - 1) + 1 : ~0ull;
+      __builtin_amdgcn_wave_barrier();
+    };
+    auto pop = [&](uint64_t& key) -> bool {
+      if (hn == 0) refill_head();
+      if (hn == 0) return false;
+      key = readlane_u64(hk, 0);
+      const uint64_t dk = wave_down1_u64(hk);
+      hk = (uint32_t)lane < hn - 1 ? dk : ~0ull;
+      hn--;
+      return true;
+    };
 
     // ---- setupDistances (exact L2) + setupSeeds (Graph.cpp:293-367) -------
     const uint64_t sb = a.seed_off ? a.seed_off[qi] : (uint64_t)qi * a.seed_stride;
@@ -955,23 +1117,13 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
       __syncthreads();
       qg_exact<PPL, NCH>(qlds, a, st.nid, st.nd, (int)m);
       __syncthreads();
-      if ((uint32_t)lane < m) {
-        const uint32_t id = st.nid[lane];
-        visit(a.ht_log2, st, id, bitmap_mode, vis, epoch);
-        const uint64_t key = make_key(st.nd[lane], packed ? a.qkw[id] : id);
-        if (ncq + lane < a.cq_cap) st.cq[ncq + lane] = key;
-        else spill[nspill + (ncq + lane - a.cq_cap)] = key;
-      }
+      if ((uint32_t)lane < m) visit(a.ht_log2, st, st.nid[lane], bitmap_mode, vis, epoch);
       __syncthreads();
       for (uint32_t j = 0; j < m; j++) {
         const float d = st.nd[j];
-        if (d <= a.radius) res_insert(st.res, nres, size, make_key(d, st.nid[j]));
-      }
-      if (ncq + m <= a.cq_cap) {
-        ncq += m;
-      } else {
-        nspill += ncq + m - a.cq_cap;
-        ncq = a.cq_cap;
+        const uint32_t id = st.nid[j];
+        insert_key(make_key(d, packed ? a.qkw[id] : id));
+        if (d <= a.radius) res_insert(st.res, nres, size, make_key(d, id));
       }
       nexact += m;
       nvisited += m;
@@ -982,64 +1134,17 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         __syncthreads();
       }
     }
-    if (nspill) spill_rebuild(spill, cmin, nspill, tmin);
     if (nres >= size) radius = key_dist(st.res[size - 1]);
-    float expr = __fmul_rn(a.coef, radius);
+    expr = __fmul_rn(a.coef, radius);
 
     // ---- best-first loop over ADC distances (QuantizedGraph.h:220-268) ----
 #ifdef NGT_AMD_STAMPS
     t_last = stamp();
 #endif
     for (;;) {
-      uint64_t best = ~0ull;
-      uint32_t bidx = 0xffffffffu;
-      for (uint32_t i = lane; i < ncq; i += 64) {
-        const uint64_t key = st.cq[i];
-        if (key < best) { best = key; bidx = i; }
-      }
-      for (uint32_t i = lane; i < ((nspill + 63) >> 6); i += 64) {
-        const uint64_t key = cmin[i];
-        if (key < best) { best = key; bidx = i | 0x80000000u; }
-      }
-      const uint64_t wbest = wave_min_u64(best);
-      if (wbest == ~0ull) break;
+      uint64_t wbest;
+      if (!pop(wbest)) break;
       if (key_dist(wbest) > expr) break;
-      const uint64_t owner = ballot64(best == wbest);
-      const int olane = __ffsll((long long)owner) - 1;
-      bidx = __shfl(bidx, olane, 64);
-      if (bidx & 0x80000000u) {
-        // the minimum is in spill chunk c: find it, move the last key into its
-        // place, refresh the minima of the chunks that changed
-        const uint32_t c = bidx & 0x7fffffffu;
-        const uint32_t i = c * 64 + lane;
-        const uint64_t k = i < nspill ? spill[i] : ~0ull;
-        const uint64_t hit = ballot64(k == wbest);
-        if (hit == 0) {
-          if (lane == 0) atomicOr(a.error, 256);
-          break;
-        }
-        const uint32_t pos = c * 64 + (uint32_t)(__ffsll((long long)hit) - 1);
-        const uint32_t last = nspill - 1;
-        const uint64_t lastkey = shfl_u64(lane == 0 ? spill[last] : 0ull, 0);
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0 && pos != last) spill[pos] = lastkey;
-        nspill = last;
-        const uint64_t mc = wave_min_u64(i < nspill ? (i == pos ? lastkey : k) : ~0ull);
-        if (lane == 0) cmin[c] = mc;
-        const uint32_t L = last >> 6;
-        uint64_t mL = mc;
-        if (L != c) {
-          mL = chunk_min(spill, L, nspill);
-          if (lane == 0) cmin[L] = mL;
-        }
-        if (nspill) {
-          const uint32_t lp = (nspill - 1) >> 6;
-          tmin = lp == c ? mc : (lp == L ? mL : chunk_min(spill, lp, nspill));
-        }
-      } else {
-        if (lane == 0) st.cq[bidx] = st.cq[ncq - 1];
-        ncq--;
-      }
       nexp++;
       NGT_MARK(t_pop);
 
@@ -1095,33 +1200,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
           // results by (distance, id); the unchecked set by (distance, key
           // word) in the packed layout -- the same order
           const uint64_t rkey = make_key(d, st.nid[base + j]);
-          const uint64_t key = packed ? make_key(d, nkw[base + j]) : rkey;
-          // keys beyond expr can never be popped; expr only shrinks, so a
-          // compaction at an unchanged expr would drop nothing
-          if (ncq >= a.cq_cap && expr != cq_cut) {
-            ncq = compact(st.cq, ncq, expr);
-            cq_cut = expr;
-          }
-          if (ncq < a.cq_cap) {
-            if (lane == 0) st.cq[ncq] = key;
-            ncq++;
-          } else {
-            if (nspill >= scap && expr != sp_cut) {
-              nspill = compact(spill, nspill, expr);
-              sp_cut = expr;
-              spill_rebuild(spill, cmin, nspill, tmin);
-            }
-            if (nspill >= scap) {
-              if (lane == 0) atomicOr(a.error, 1);
-            } else {
-              tmin = (nspill & 63) == 0 ? key : (key < tmin ? key : tmin);
-              if (lane == 0) {
-                spill[nspill] = key;
-                cmin[nspill >> 6] = tmin;
-              }
-              nspill++;
-            }
-          }
+          insert_key(packed ? make_key(d, nkw[base + j]) : rkey);
           if (d <= radius) {
             res_insert(st.res, nres, size, rkey);
             if (nres >= size) {
@@ -1136,7 +1215,6 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         const uint32_t na = (uint32_t)__popcll(acc);
         nacc += na;
         nvisited += na;
-        if (ncq + nspill > maxq) maxq = ncq + nspill;
         __syncthreads();
         if (!bitmap_mode && nvisited > hlimit) {
           ht_to_vis(a.ht_log2, st, vis, epoch);
@@ -1268,6 +1346,7 @@ size_t qg_search_lds_bytes(const QgSearchArgs& a) {
   b += 2 * (((size_t)8 * (a.size + 1) + 15) & ~(size_t)15);
   const uint32_t nstage = a.id_stride > a.size ? a.id_stride : a.size;
   b += (size_t)12 * ((nstage + 63) & ~63u);
+  b += 256 + 512;  // threshold-selection counters and staged keys
   b += (size_t)a.dp * 4;
   return b;
 }

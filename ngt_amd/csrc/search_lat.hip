@@ -48,6 +48,7 @@ struct LatCtl {
   uint32_t k;     // this query's SearchContainer::size, coefficient, radius
   float coef;
   float radius;
+  float expr;     // the commit wave's exploration radius (read by the hop prefetch)
   uint32_t ns;    // serving form: seeds staged in the tail
   uint64_t sp[4]; // diagnostic build: speculation-wave cycles ([0] adjacency, [2] exact rows)
 };
@@ -86,6 +87,16 @@ struct LatLayout {
 };
 
 __device__ __forceinline__ bool bm_test(const uint32_t* bm, uint32_t id) { return (bm[id >> 5] >> (id & 31)) & 1u; }
+
+__device__ __forceinline__ float wave_min_f32(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float lds_load_f32(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP));
+}
 
 __device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -331,7 +342,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       float radius = radq;
       uint32_t qerr = 0;  // the batch kernel's error bits, this query's
       float expr = 0.f;
-      auto set_expr = [&]() { expr = __fmul_rn(coefq, radius); };
+      auto set_expr = [&]() {
+        expr = __fmul_rn(coefq, radius);
+        if (lane == 0) ctl->expr = expr;
+      };
       // unchecked set: head (registers, sorted, hn keys) < B <= tail (LDS,
       // ntail keys) < T <= spill (HBM, nspill keys)
       uint64_t hk = ~0ull;
@@ -864,6 +878,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         // the comparator's exact distances of those neighbours
         // (PrimitiveComparator::compareL2 through l2_fold_rows): a quad per
         // row, EG groups of 16 rows in flight
+        float hop_d = __int_as_float(0x7f800000);  // this lane's nearest fresh neighbour
+        uint32_t hop_id = 0u;
         {
           const float4* qq = reinterpret_cast<const float4*>(qlds) + g;
           for (uint32_t r0 = 0; r0 < np; r0 += 16u * EG) {
@@ -884,7 +900,13 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
               if (r0 + 16u * j >= np) continue;
               const uint32_t rr = r0 + 16u * j + (uint32_t)rs;
               const float d = l2_fold_rows<NCH>(qq, v[j]);
-              if (g == 0 && rr < np) sd[rr] = d;
+              if (g == 0 && rr < np) {
+                sd[rr] = d;
+                if (d < hop_d) {
+                  hop_d = d;
+                  hop_id = rid[j];
+                }
+              }
             }
           }
         }
@@ -901,6 +923,29 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         // bit is set, the commit wave may free and reissue it
         if (lane == 0)
           __hip_atomic_fetch_or(&slots[sl].pready, 1u << part, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // hop prefetch.  The commit wave waits on memory when it pops a node
+        // nobody has speculated -- typically one its previous expansion just
+        // accepted, i.e. the nearest neighbour of a list like this one.  The
+        // part's nearest fresh neighbour within the exploration radius is
+        // therefore read ahead: its adjacency row, then one word of every
+        // 128-byte line of its fresh neighbours' rows, so that when it is
+        // issued its own speculation's two round trips hit L2.  Nothing is
+        // stored: results cannot change, only where the later loads hit.
+        if (a.lat_hop) {
+          const float hd = wave_min_f32(g == 0 ? hop_d : __int_as_float(0x7f800000));
+          const uint64_t hm = ballot64(g == 0 && hop_d == hd && hop_id != 0u);
+          if (hm != 0ull && hd <= lds_load_f32(&ctl->expr)) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)hop_id, __ffsll((long long)hm) - 1);
+            const uint32_t wl = cap < 64u ? cap : 64u;
+            const uint32_t nb = (uint32_t)lane < wl ? a.adj[(uint64_t)w * a.adj_stride + lane] : 0u;
+            uint32_t acc = 0u;
+            if (nb != 0u && !bm_test(bm, nb)) {
+              const uint32_t* x = reinterpret_cast<const uint32_t*>(a.rows + (uint64_t)nb * a.row_bytes);
+              for (uint32_t l = 0; l < (uint32_t)a.row_bytes / 128u; l++) acc += x[32u * l];
+            }
+            asm volatile("" ::"v"(acc));
+          }
+        }
       }
     }
     __syncthreads();
