@@ -106,7 +106,12 @@ struct SearchArgs {
   // within the exploration radius (the predicted rest of its search); a query
   // that ends first writes its results and qflag[qi] = 2.  A later launch
   // resumes the paused queries (qflag 1) from their saved state, longest
-  // predicted first.  Results are the same in any order and split.
+  // predicted first.  Results, distance bits and expansion / edge counts are
+  // the single launch's in any order and split; the evaluation counters
+  // ([0], [1], [6]) may be higher: the resume rebuilds the accepted-only set
+  // from the popped ids and the unchecked keys, and accepted ids that a
+  // compaction had dropped beyond the radius are evaluated (and rejected)
+  // again.  The bench takes U(q) from a full-visited-set run, never scheduled.
   const uint32_t* order;
   const uint32_t* nwork_dev;
   uint32_t pause_after;

@@ -59,6 +59,9 @@ def test_probe_and_resume_identical(monkeypatch, budget, cq):
         assert np.array_equal(ad.view(np.uint32), bd.view(np.uint32))
         for c in (2, 4):  # expansions, edges read: the same traversal
             assert np.array_equal(ac[:, c], bc[:, c]), (eps, c)
+        # evaluations: never fewer; more only where a resume re-evaluated an
+        # accepted id that compaction had dropped (ngt_kernels.h SearchArgs)
+        assert (bc[:, 0] >= ac[:, 0]).all(), eps
         assert (bc[:, 2] > budget).any()  # some queries were paused and resumed
         for i in range(0, len(qs), 97):
             oi, od, _ = O.search("l2", rows, offs, edges, qs[i], seeds[i], 10, np.float32(eps))
