@@ -11,3 +11,11 @@ for cfg in "128 48 96 160" "128 32 96 128" "128 24 96 120" "128 16 112 128" "128
     || { tail -20 $O/$n.log; exit 1; }
   python3 scripts/jline.py $O/$n.json $n
 done
+for s in 4 5; do
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --anng-line off --c3-line off --no-cpu \
+    --latency-queries 0 --streams $s > $O/streams$s.json 2> $O/streams$s.log || { tail -20 $O/streams$s.log; exit 1; }
+  python3 scripts/jline.py $O/streams$s.json streams$s
+done
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --anng-line off --c3-line off --no-cpu \
+  --latency-queries 0 --streams 3 > $O/streams3.json 2> $O/streams3.log || { tail -20 $O/streams3.log; exit 1; }
+python3 scripts/jline.py $O/streams3.json streams3
