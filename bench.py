@@ -340,10 +340,15 @@ def main():
     ap.add_argument("--seeds", choices=["random", "tree"], default=None,
                     help="random: getRandomSeeds (graph-only search); tree: the DVP tree's leaf "
                          "(GraphAndTreeIndex::search, `ngt search`'s default); default tree for --graph anng")
-    ap.add_argument("--knn", type=int, default=128)
-    ap.add_argument("--out-deg", type=int, default=48)
-    ap.add_argument("--in-deg", type=int, default=96)
-    ap.add_argument("--max-deg", type=int, default=160)
+    # the kNN surrogate graph (build_graph): kNN256 -> 64 out + 224 in edges,
+    # <= 256 per node (the padded adjacency's limit).  Round 5's sweep
+    # (profiles/r5e, r5k, r5l): denser graphs need fewer expansions for the same
+    # recall (C2: 327 vs 576 per query, 16.2 vs 18.7 ms per search than kNN128
+    # out48 in96 max160)
+    ap.add_argument("--knn", type=int, default=256)
+    ap.add_argument("--out-deg", type=int, default=64)
+    ap.add_argument("--in-deg", type=int, default=224)
+    ap.add_argument("--max-deg", type=int, default=256)
     ap.add_argument("--seed-size", type=int, default=10)
     ap.add_argument("--eps", type=str, default="")
     ap.add_argument("--expansion", type=float, default=3.0, help="NGTQG result_expansion")

@@ -405,14 +405,15 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   a.cq_cap = 1024;
   a.vf_log2 = 0;
   if (prm->visited_hash_log2 < 0) {
-    // HBM epochs.  A 512-key unchecked array compacts dead keys twice as
-    // often, so pops scan fewer (+6 % QPS on the C2-graph NGTQG bench, same
-    // results).  The 16 Kbit LDS filter of accepted ids (~1.7k per query)
-    // lets ids_and_adc probe the few possibly-visited neighbours while the
-    // ADC runs, instead of a round trip in the accept step.
+    // HBM epochs behind an LDS filter of accepted ids, which lets ids_and_adc
+    // probe the possibly-visited neighbours while the ADC runs instead of a
+    // round trip in the accept step.  With the register head the LDS tail
+    // needs only 256 keys, and their room buys a 32 Kbit filter: fewer false
+    // positives, fewer probes (round 5, profiles/r5k / r5l: 2M one-ANNG QG
+    // +5.6 %, C2-graph QG +3 %; 64 Kbit costs resident waves and loses).
     a.ht_log2 = 0;
-    a.cq_cap = 512;
-    a.vf_log2 = 14;
+    a.cq_cap = 256;
+    a.vf_log2 = 15;
   }
   else if (prm->visited_hash_log2 > 0) a.ht_log2 = (uint32_t)std::max(8, std::min(15, prm->visited_hash_log2));
   if (const char* v = ngt_amd::knob("NGT_AMD_HT_LOG2")) a.ht_log2 = (uint32_t)std::max(8, std::min(15, atoi(v)));
