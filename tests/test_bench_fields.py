@@ -1,0 +1,30 @@
+"""bench.py's roofline fields (CPU): SURVEY.md 8(d)'s literal bytes, the
+Infinity-Cache-resident share and the counter-based bound label."""
+import numpy as np
+
+import bench
+
+
+def test_literal_bytes_exact_and_qg():
+    # counters [q, 8]: c[0] distances, c[4] edges (exact) / code blocks (qg), c[3] exact distances (qg)
+    c = np.zeros((3, 8))
+    c[:, 0] = [100, 200, 300]
+    c[:, 4] = [10, 20, 30]
+    c[:, 3] = [5, 5, 5]
+    dp, nq, k = 128, 3, 10
+    assert bench.literal_bytes(c, dp, nq, k, False, 128) == 600 * dp * 4 + 60 * 4 + nq * (dp * 4 + k * 8)
+    # NGTQG: blocks * 8 * Me + ADC distances * 4 + exact rows * Dp * 4 + per query Dp * 4 + k * 8
+    assert bench.literal_bytes(c, dp, nq, k, True, 128) == 60 * 8 * 128 + 600 * 4 + 15 * dp * 4 + nq * (dp * 4 + k * 8)
+
+
+def test_ic_share():
+    assert bench.ic_share(None, 100.0) == 0.0
+    assert bench.ic_share({"filter_copy_fits_infinity_cache": False, "filter_copy_bytes": 50.0}, 100.0) == 0.0
+    assert bench.ic_share({"filter_copy_fits_infinity_cache": True, "filter_copy_bytes": 88.0}, 100.0) == 0.88
+
+
+def test_bound_from_counters():
+    w = 1000.0
+    assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 560, "SQ_ACTIVE_INST_VALU": 100}) == "latency"
+    assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 300, "SQ_ACTIVE_INST_VALU": 600}) == "valu"
+    assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 300, "SQ_ACTIVE_INST_VALU": 100}) == "hbm"
