@@ -807,6 +807,23 @@ def main():
                 "feed %.3g (sum %.3g); never handed out %.0f; speculation waves (summed): adjacency %.3g "
                 "filter %.3g exact %.3g" % (tot[0], tot[1], tot[2], tot[3], tot.sum(), lcc[:, 3].mean(),
                                             sp[0], sp[1], sp[2]))
+        if args.seeds == "tree" and args.edge_size == -1:
+            # the same queries answered by the resident serving grid (what a
+            # lone ngt_search_index call gets): host wall time per call
+            served = []
+            for i in range(args.latency_queries):
+                t1 = time.perf_counter()
+                r = ix.search_served(qry[i], k=K, epsilon=chosen)
+                served.append(time.perf_counter() - t1)
+                if r is None:
+                    served = []
+                    break
+            if served:
+                sv = np.array(served[1:] if len(served) > 1 else served) * 1e3
+                latency["served_mean_ms"] = float(sv.mean())
+                latency["served_p50_ms"] = float(np.percentile(sv, 50))
+                log("single queries through the serving grid: mean %.3f ms p50 %.3f" % (
+                    latency["served_mean_ms"], latency["served_p50_ms"]))
 
     cpu = parity = None
     if rank == 0 and not args.no_cpu and world == 1 and not shard:
