@@ -739,7 +739,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   // features do not predict the cost (centroid distance, sampled distance
   // contrast: rank correlation < 0.1); the search's own state does: the
   // unchecked keys within the exploration radius after part of the search.
-  // So a probe launch runs every query for B expansions (B = 0.12 x the mean
+  // So a probe launch runs every query for B expansions (B = 0.25 x the mean
   // expansions per query of earlier launches of this configuration) and
   // pauses the unfinished ones with their state saved; a one-workgroup
   // counting sort orders them by that count; a resume launch continues them
@@ -747,9 +747,12 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
   // set from the popped ids and the unchecked keys; search_kernels.hip), so
   // the results, distance bits and expansion counts are the single
   // launch's.  Measured (profiles/r4e, r4f): C2 22.2 -> 18.6 ms per 10k-query
-  // search at 0.12 (19.4 at 0.25, 20.2 at 0.4).  The lookahead kernel (the
-  // ANNG's short lists) took the same scheme and ran slower at every
-  // fraction (0.08-0.5: 164-174 ms against 156), so it is not scheduled.
+  // search at 0.12 (19.4 at 0.25, 20.2 at 0.4) on the kNN128 graph; on the
+  // denser kNN256 graph (327 expansions per query, profiles/r5o, r5p) 16.3 /
+  // 16.2 / 15.4 / 15.4 / 15.1 / 15.3 ms at 0.06 / 0.12 / 0.2 / 0.25 / 0.3 /
+  // 0.4.  The lookahead kernel (the ANNG's short lists) took the same scheme
+  // and ran slower at every fraction (0.08-0.5: 164-174 ms against 156), so
+  // it is not scheduled.
   const bool sched_shape = !lat && la_mode < 0 && a.accepted_only && a.ht_log2 == 0 && a.vf_log2 != 0 && a.adj &&
                            a.fcodes && a.k <= 64;
   uint32_t budget = 0;
@@ -764,7 +767,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       if (m.first == skey) mean = m.second;
     static const double frac = [] {
       const char* v = ngt_amd::knob("NGT_AMD_SCHED_FRAC");
-      return v ? std::max(0.01, std::min(0.9, atof(v))) : 0.12;
+      return v ? std::max(0.01, std::min(0.9, atof(v))) : 0.25;
     }();
     // test knob: a fixed budget for every eligible launch
     const int forced = ngt_amd::knob("NGT_AMD_SCHED_B") ? std::max(0, atoi(ngt_amd::knob("NGT_AMD_SCHED_B"))) : 0;

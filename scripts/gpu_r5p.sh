@@ -13,3 +13,8 @@ print("c2", round(d["value"]), "shard", round(s["value"]), s["config"]["recall_a
       s["config"]["shards_per_gpu"], round(s["roofline"]["kernel_ms"], 2), round(s["roofline"]["frac"], 3),
       s["parity_sample"], round(s["wall_s"]), s["config"]["setup_s"])
 PY
+for f in 0.25 0.3 0.4; do
+  NGT_AMD_TEST_KNOBS=1 NGT_AMD_SCHED_FRAC=$f timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --anng-line off \
+    --c3-line off --no-cpu --latency-queries 0 > $O/frac$f.json 2> $O/frac$f.log || { tail -20 $O/frac$f.log; exit 1; }
+  python3 scripts/jline.py $O/frac$f.json frac$f
+done

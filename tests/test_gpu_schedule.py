@@ -72,7 +72,7 @@ def test_probe_and_resume_identical(monkeypatch, budget, cq):
 
 def test_schedule_from_earlier_launches(monkeypatch):
     """Without a forced budget the second launch of a configuration takes a
-    eighth of the first one's mean expansions per query (a launch with more
+    quarter of the first one's mean expansions per query (a launch with more
     queries than slots); results stay identical."""
     monkeypatch.setenv("NGT_AMD_LA", "0")
     monkeypatch.delenv("NGT_AMD_SCHED_B", raising=False)
@@ -83,7 +83,7 @@ def test_schedule_from_earlier_launches(monkeypatch):
     bi, bd, bn, bc = _search(ix, qs, seeds, 0.2)
     if len(qs) * 4 >= slots * 5:
         mean = ac[:, 2].astype(np.float64).mean()
-        assert ix.last_search_budget() == max(8, int(mean * 0.12))
+        assert ix.last_search_budget() == max(8, int(mean * 0.25))
     assert np.array_equal(ai, bi) and np.array_equal(an, bn)
     assert np.array_equal(ad.view(np.uint32), bd.view(np.uint32))
     assert np.array_equal(ac[:, 2], bc[:, 2])
