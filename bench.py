@@ -801,12 +801,11 @@ def main():
             log("single-query: %.0f expansions, %.0f of them waited for their list" % (
                 lcc[:, 2].mean(), lcc[:, 3].mean()))
         else:
-            tot = lcc[:, [5, 6, 1, 7]].mean(0)
+            tot = lcc[:, [5, 6, 1, 3, 7]].mean(0)
             sp = lcc[:, [0, 4, 2]].mean(0)
-            log("single-query phase cycles (latency kernel): commit wave: pop %.3g wait %.3g list+accept %.3g "
-                "feed %.3g (sum %.3g); never handed out %.0f; speculation waves (summed): adjacency %.3g "
-                "filter %.3g exact %.3g" % (tot[0], tot[1], tot[2], tot[3], tot.sum(), lcc[:, 3].mean(),
-                                            sp[0], sp[1], sp[2]))
+            log("single-query phase cycles (latency kernel): commit wave: pop %.3g wait %.3g list+visited %.3g "
+                "accept %.3g feed %.3g (sum %.3g); speculation waves (summed): adjacency %.3g filter %.3g "
+                "exact %.3g" % (tot[0], tot[1], tot[2], tot[3], tot[4], tot.sum(), sp[0], sp[1], sp[2]))
         if args.seeds == "tree" and args.edge_size == -1:
             # the same queries answered by the resident serving grid (what a
             # lone ngt_search_index call gets): host wall time per call

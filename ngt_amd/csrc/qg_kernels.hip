@@ -709,7 +709,8 @@ template <int PPL, int NB>
 __device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, const uint8_t* rec, uint32_t nb,
                                                        uint32_t Me, float scale, float toff, uint32_t* nid,
                                                        uint32_t* nkw, float* dists, bool probe, const SearchState& st,
-                                                       const uint8_t* vis, uint32_t epoch, uint64_t (&seen)[2]) {
+                                                       const uint8_t* vis, uint32_t epoch, float expr,
+                                                       uint64_t (&seen)[2]) {
   const int lane = lane_id();
   const uint32_t npairs = Me >> 1;
   const uint64_t blk = (uint64_t)8 * Me;
@@ -743,21 +744,11 @@ __device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, co
     }
     deg += (uint32_t)__popcll(ballot64(e.x != 0u));
   }
-  bool pre[NC];
-  uint32_t word[NC];
-#pragma unroll
-  for (int cc = 0; cc < NC; cc++) {
-    pre[cc] = false;
-    word[cc] = 0;
-    if (probe && idr[cc] != 0u) {
-      const uint32_t b = (idr[cc] * 0x85EBCA77u) >> st.vf_shift;
-      pre[cc] = (st.vf[b >> 5] >> (b & 31)) & 1u;
-      if (pre[cc])
-        word[cc] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (idr[cc] & ~3u)), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   const uint32_t nbd = deg == 0 ? 0 : (deg - 1) / 16 + 1;
+  // lane l's entries' ADC distances (entry 64 * cc + l)
+  float dv[NC];
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) dv[cc] = __int_as_float(0x7f800000);
 #if NGT_AMD_QG_VALU_REDUCE
 #pragma unroll
   for (int j = 0; j < NB; j++) {
@@ -769,8 +760,13 @@ __device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, co
       if ((lane & 3) == 0 && o < deg) dists[o] = adc_epilogue(r, scale, toff);
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++)
+    if (64u * cc + lane < deg) dv[cc] = dists[64u * cc + lane];
 #else
   const uint32_t base = 0x03020100u;
+  static_assert((NB + 3) / 4 == NC, "ADC pass q covers entries 64q..64q+63");
 #pragma unroll
   for (int q = 0; q < (NB + 3) / 4; q++) {
     if ((uint32_t)(4 * q) < nbd) {
@@ -783,10 +779,31 @@ __device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, co
       }
       const uint32_t r = fold4(part[0], part[1], part[2], part[3]);
       const uint32_t o = (uint32_t)(4 * q) * 16 + (uint32_t)lane;
-      if (o < deg) dists[o] = adc_epilogue_total(r, Me, scale, toff);
+      if (o < deg) {
+        dv[q] = adc_epilogue_total(r, Me, scale, toff);
+        dists[o] = dv[q];
+      }
     }
   }
 #endif
+  // the visited probe, after the ADC: only an entry within the exploration
+  // radius can be accepted (the accept step tests `d <= expr` with an expr
+  // that only shrinks), so only those whose filter bit is set read their
+  // epoch word -- the others' seen bits are never looked at
+  bool pre[NC];
+  uint32_t word[NC];
+#pragma unroll
+  for (int cc = 0; cc < NC; cc++) {
+    pre[cc] = false;
+    word[cc] = 0;
+    if (probe && idr[cc] != 0u && dv[cc] <= expr) {
+      const uint32_t b = (idr[cc] * 0x85EBCA77u) >> st.vf_shift;
+      pre[cc] = (st.vf[b >> 5] >> (b & 31)) & 1u;
+      if (pre[cc])
+        word[cc] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(vis + (idr[cc] & ~3u)), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   seen[0] = seen[1] = 0;
 #pragma unroll
   for (int cc = 0; cc < NC; cc++)
@@ -1160,7 +1177,7 @@ __global__ void __launch_bounds__(64, 4) ngt_qg_search_kernel(QgSearchArgs a) {
         const uint8_t* rec = a.recs + ((uint64_t)(target >> 3) << a.rec_shift);
         deg = ids_and_adc_packed<PPL, (NB > 0 ? NB : 1)>(L, rec, (target & 7u) + 1u, a.Me, scale, toff, st.nid, nkw,
                                                          st.nd, !use_hash && st.vf != nullptr, st, vis, epoch,
-                                                         seen_pre);
+                                                         expr, seen_pre);
         NGT_MARK(t_ids);
       } else if (early) {
         deg = ids_and_adc<PPL, (NB > 0 ? NB : 1)>(L, nbr, a.id_stride, a.qcodes + (uint64_t)target * a.code_stride,

@@ -127,7 +127,12 @@ __device__ void serve_dispatch(const ServeArgs& sv) {
     else if (now - t0 > sv.life_ticks) why = 3;
     if (why) break;
     const ServeReqHdr* h = reinterpret_cast<const ServeReqHdr*>(sv.ring + (uint64_t)(avail % sv.nring) * sv.req_bytes);
-    if (__hip_atomic_load(&h->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == avail + 1u) {
+    // polled relaxed, acquired once per ticket: an acquire at agent or
+    // system scope invalidates caches, and a poll loop issuing one every few
+    // hundred cycles would keep flushing the lines the searching workers of
+    // this XCD are warming
+    if (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == avail + 1u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       avail++;
       __hip_atomic_store(&sv.dctl->avail, avail, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       last = now;
@@ -144,10 +149,12 @@ __device__ void serve_dispatch(const ServeArgs& sv) {
 // final.  Workers also leave on their own after life + idle + 1 s, so a grid
 // whose dispatcher block never got a CU still drains.
 __device__ bool serve_claim(const ServeArgs& sv, uint64_t t0, uint32_t& ticket) {
-  // idle workers back off (all of them poll the same control line)
+  // idle workers back off (all of them poll the same control line); the polls
+  // are relaxed, as in serve_dispatch: the successful claim's CAS is the
+  // acquire, and it reads `avail`'s release by the dispatcher
   for (uint32_t idle = 0;; idle++) {
     uint32_t c = __hip_atomic_load(&sv.dctl->claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t av = __hip_atomic_load(&sv.dctl->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t av = __hip_atomic_load(&sv.dctl->avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((int32_t)(av - c) > 0) {
       if (__hip_atomic_compare_exchange_strong(&sv.dctl->claimed, &c, c + 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
@@ -156,7 +163,8 @@ __device__ bool serve_claim(const ServeArgs& sv, uint64_t t0, uint32_t& ticket) 
       }
       continue;
     }
-    if (__hip_atomic_load(&sv.dctl->closing, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+    if (__hip_atomic_load(&sv.dctl->closing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const uint32_t av2 = __hip_atomic_load(&sv.dctl->avail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t c2 = __hip_atomic_load(&sv.dctl->claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((int32_t)(av2 - c2) > 0) continue;
@@ -337,8 +345,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       uint32_t ndist = 0, nexp = 0, nedge = 0, nexact = 0, nwait = 0, ns = 0, nstall = 0;
       (void)nwait;
       // diagnostic build only: shader-clock totals per phase
-      uint64_t t_pop = 0, t_wait = 0, t_list = 0, t_feed = 0, t_last = 0;
-      (void)t_pop; (void)t_wait; (void)t_list; (void)t_feed; (void)t_last;
+      uint64_t t_pop = 0, t_wait = 0, t_list = 0, t_acc = 0, t_feed = 0, t_last = 0;
+      (void)t_pop; (void)t_wait; (void)t_list; (void)t_acc; (void)t_feed; (void)t_last;
       float radius = radq;
       uint32_t qerr = 0;  // the batch kernel's error bits, this query's
       float expr = 0.f;
@@ -740,6 +748,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           const uint32_t half = (uint32_t)lane >> 5, sub = (uint32_t)lane & 31u;
 #pragma unroll 1
           for (uint32_t p = 0; p < parts; p += 2) {
+            NGT_MARK(t_list);
             for (uint32_t spin = 0; (lds_load_acq(&slots[tag].pready) & pmask(p)) != pmask(p); spin++) {
               if (spin > (1u << 24)) {
                 qerr |= 16u;
@@ -749,6 +758,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
               __builtin_amdgcn_s_sleep(1);
             }
             if (stuck) break;
+            NGT_MARK(t_wait);
             const uint32_t pp = p + half;
             const uint32_t np = pp < parts ? slots[tag].pn[pp] : 0u;
             const bool in = sub < np;
@@ -761,8 +771,11 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
             nexact += nf;
             const uint64_t km = ballot64(f && dv <= expr);
             if (km) {
+              NGT_MARK(t_list);
               accept_reg(km, idv, dv);
+              NGT_MARK(t_acc);
               if (p + 2u < parts) feed();
+              NGT_MARK(t_feed);
             }
           }
         }
@@ -780,15 +793,16 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       // ---- results (moveFrom: ascending (distance, id), ObjectSpace.h:49-57)
       uint64_t cv[8] = {ndist, ndist - ns, nexp, nstall, nedge, maxq, nexact, ns};
 #ifdef NGT_AMD_STAMPS
-      // phase cycles: [5] pop (+ refills, issue), [6] wait for the list,
-      // [1] list + accept, [7] feeding the speculation; [3] nwait; the
-      // speculation waves' sums: [0] adjacency + visited pre-test, [2] exact rows
+      // phase cycles: [5] pop (+ refills, issue), [6] waits for list parts,
+      // [1] list reads + visited test and mark, [3] accepts, [7] feeding the
+      // speculation; the speculation waves' sums: [0] adjacency + visited
+      // pre-test, [2] exact rows
       __builtin_amdgcn_s_waitcnt(0);
       cv[5] = t_pop;
       cv[6] = t_wait;
       cv[1] = t_list;
       cv[7] = t_feed;
-      cv[3] = nwait;
+      cv[3] = t_acc;
       cv[0] = ctl->sp[0];
       cv[4] = ctl->sp[1];
       cv[2] = ctl->sp[2];
