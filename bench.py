@@ -315,7 +315,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--mode", choices=["exact", "qg", "shard", "capi"], default="exact")
-    ap.add_argument("--threads", type=int, default=32, help="--mode capi: concurrent C-API callers")
+    ap.add_argument("--threads", type=int, default=64,
+                    help="C-API lines: concurrent callers T (runs at 1, T and 2T threads; the serving grid has 128 "
+                         "workers)")
     ap.add_argument("--qg", action="store_true", help="with --mode shard: NGTQG shards (C5's form)")
     ap.add_argument("--config", choices=["c2", "c3"], default="c2")
     ap.add_argument("--n", type=int, default=0, help="objects (per shard in --mode shard)")

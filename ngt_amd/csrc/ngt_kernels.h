@@ -211,12 +211,10 @@ inline uint32_t la_targets(int mode) {
 inline int la_wpe() { return 4; }
 // latency kernel: hop prefetch of each list part's nearest fresh neighbour
 // (search_lat.hip); NGT_AMD_LAT_HOP=0 turns it off (A/B)
+// (read per launch, so a test process can compare both forms)
 inline uint32_t lat_hop_default() {
-  static const uint32_t v = [] {
-    const char* e = ngt_amd::knob("NGT_AMD_LAT_HOP");
-    return e ? (atoi(e) != 0 ? 1u : 0u) : 1u;
-  }();
-  return v;
+  const char* e = ngt_amd::knob("NGT_AMD_LAT_HOP");
+  return e ? (atoi(e) != 0 ? 1u : 0u) : 1u;
 }
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 uint32_t search_lat_lds_bytes(const SearchArgs& a);

@@ -62,7 +62,6 @@ struct LatSlot {
   uint32_t claim;
   uint32_t pready; // parts finished (bit p: part p's entries and count are final)
   uint32_t deg;    // list length read (getEdgeSize cap), summed over the parts
-  uint32_t gen;    // issue generation (the commit wave's)
   uint32_t pn[8];  // neighbours not yet visited when the part was read
 };
 
@@ -299,7 +298,6 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       for (uint32_t i = tid; i < nslots; i += NT) {
         slots[i].state = kFree;
         slots[i].claim = 0u;
-        slots[i].gen = 0u;
         slots[i].pready = 0u;
       }
       if (tid == 0) {
@@ -361,6 +359,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       uint32_t hn = 0, ntail = 0, nspill = 0;
       uint64_t B = ~0ull, T = ~0ull;
       uint64_t freem = nslots >= 64 ? ~0ull : ((1ull << nslots) - 1ull);  // free slots
+      uint32_t sgen = 0u;  // lane s: slot s's issue generation (only this wave issues)
       uint64_t orphan = 0ull;                                             // issued, no longer in the head
       const uint32_t F = nslots < 16u ? nslots : 16u;                     // head entries kept speculated
 
@@ -609,17 +608,18 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         const uint32_t s = (uint32_t)(__ffsll((long long)freem) - 1);
         freem &= ~(1ull << s);
-        const uint32_t gen = (slots[s].gen + 1u) & 0xffffffu;
+        const uint32_t gen = ((uint32_t)__builtin_amdgcn_readlane((int)sgen, (int)s) + 1u) & 0xffffffu;
+        if ((uint32_t)lane == s) sgen = gen;
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
           slots[s].key = key;
           slots[s].pready = 0u;
           slots[s].deg = 0u;
-          slots[s].gen = gen;
         }
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
-          lds_store_rel(&slots[s].claim, gen << 8);
+          // the state's release publishes the claim word with the rest
+          __hip_atomic_store(&slots[s].claim, gen << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           lds_store_rel(&slots[s].state, kIssued);
         }
         return s;
@@ -732,8 +732,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         // each pass waits only for its own two parts: the first parts of a
         // list are applied (and their accepts handed out) while the later
         // ones are still in flight
-        if ((lds_load_acq(&slots[tag].pready) & pmask(0u)) != pmask(0u)) nstall++;
+        uint32_t pr = lds_load_acq(&slots[tag].pready);  // reused by the first pass
+        if ((pr & pmask(0u)) != pmask(0u)) nstall++;
         NGT_MARK(t_wait);
+        uint32_t dg = 0u;  // the list length read, final once every part is
         nexp++;
         // the parts of the list in order, two per pass (lanes 0-31 part p,
         // 32-63 part p+1; each part compacted in list order, so lane order
@@ -749,7 +751,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
 #pragma unroll 1
           for (uint32_t p = 0; p < parts; p += 2) {
             NGT_MARK(t_list);
-            for (uint32_t spin = 0; (lds_load_acq(&slots[tag].pready) & pmask(p)) != pmask(p); spin++) {
+            for (uint32_t spin = 0; (pr & pmask(p)) != pmask(p); spin++) {
+              pr = lds_load_acq(&slots[tag].pready);
+              if ((pr & pmask(p)) == pmask(p)) break;
               if (spin > (1u << 24)) {
                 qerr |= 16u;
                 stuck = true;
@@ -760,10 +764,15 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
             if (stuck) break;
             NGT_MARK(t_wait);
             const uint32_t pp = p + half;
+            // the entries are read with the count, not after it (one LDS
+            // round trip; lanes past the count discard theirs)
+            const uint32_t rid = pp < parts ? sid[pp * span + sub] : 0u;
+            const float rdv = pp < parts ? sd[pp * span + sub] : 0.f;
             const uint32_t np = pp < parts ? slots[tag].pn[pp] : 0u;
+            if (p + 2u >= parts) dg = slots[tag].deg;  // the last pass: every part is final
             const bool in = sub < np;
-            const uint32_t idv = in ? sid[pp * span + sub] : 0u;
-            const float dv = in ? sd[pp * span + sub] : 0.f;
+            const uint32_t idv = in ? rid : 0u;
+            const float dv = in ? rdv : 0.f;
             const bool f = idv != 0u && !bm_test(bm, idv);
             if (f) atomicOr(bm + (idv >> 5), 1u << (idv & 31));
             const uint32_t nf = (uint32_t)__popcll(ballot64(f));
@@ -780,7 +789,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
           }
         }
         if (stuck) break;
-        nedge += slots[tag].deg;
+        nedge += dg;
         release_slot(tag);
         NGT_MARK(t_list);
         feed();

@@ -162,3 +162,37 @@ def test_latency_kernel_spill_and_slots(monkeypatch, knobs, deg):
         assert np.array_equal(cnt[:, 0], oc[:, 0].astype(np.uint64)), eps
         assert np.array_equal(cnt[:, 2], oc[:, 2].astype(np.uint64)), eps
     ix.close()
+
+
+@pytest.mark.parametrize("hop", ["0", "1"])
+@pytest.mark.parametrize("deg", [24, 40, 150])
+def test_latency_kernel_hop_forms(monkeypatch, hop, deg):
+    """The latency kernel's hop prefetch -- each list part's nearest fresh
+    neighbour read towards L2 by the speculation wave (1, the default) or not
+    (0) -- leaves ids, distance bits and the reference's distance/expansion
+    counts unchanged, also with two slots (issued, orphaned and re-issued
+    head entries)."""
+    monkeypatch.setenv("NGT_AMD_LA", "2")
+    monkeypatch.setenv("NGT_AMD_LAT_HOP", hop)
+    n, dim = 6000, 128
+    rows, offs, edges = _graph(n, dim, deg, 91 + deg)
+    ix = DeviceIndex("l2", "float", dim)
+    ix.set_objects(rows)
+    ix.set_graph(offs, edges)
+    rng = np.random.default_rng(deg + 3)
+    qs = rng.random((12, dim), dtype=np.float32)
+    seeds = [rng.choice(np.arange(1, n), 10, replace=False).astype(np.uint32) for _ in range(12)]
+    for slots, eps in (("", 0.1), ("", 0.4), ("2", 0.2)):
+        if slots:
+            monkeypatch.setenv("NGT_AMD_LAT_SLOTS", slots)
+        gi, gd, gn, cnt = ix.search(qs, k=20, epsilon=eps, edge_size=0, seed_mode=SEED_GIVEN, seeds=seeds)
+        assert ix.last_search_lookahead() == 1
+        oi, od, on, oc = O.search_batch("l2", rows, offs, edges, qs, seeds, 20, np.float32(eps), edge_size=0,
+                                        threads=os.cpu_count() or 1)
+        assert np.array_equal(gn, on)
+        for i in range(12):
+            assert list(gi[i, :gn[i]]) == list(oi[i, :on[i]]), (eps, i)
+            assert np.array_equal(gd[i, :gn[i]].view(np.uint32), od[i, :on[i]].view(np.uint32)), (eps, i)
+        for c in (0, 2):
+            assert np.array_equal(cnt[:, c], oc[:, c].astype(np.uint64)), (eps, c)
+    ix.close()
