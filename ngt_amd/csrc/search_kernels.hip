@@ -205,8 +205,19 @@ __device__ __forceinline__ void pause_restore(const uint8_t* prec, const PauseLa
   __syncthreads();
 }
 
+// Waves per SIMD: 4 (128 VGPRs) for the register-row L2 form and long L2
+// rows; 3 (168 VGPRs) for long cosine/angle rows (C3), whose filter bound and
+// comparator want ~214 and spilled 260 B per lane at 128 -- 758-761 ms per
+// C3 launch against 824-828 at 4 and 857-859 at 2 (profiles/r5zc, one box)
+#ifndef NGT_AMD_C2_WPE
+#define NGT_AMD_C2_WPE 4
+#endif
+template <int M, int NCH, int G>
+constexpr int search_waves_per_simd() {
+  return (NCH > 0 && G == 1) ? NGT_AMD_C2_WPE : (NCH < 0 ? (M == kL2 ? 4 : 3) : 2);
+}
 template <int M, typename T, int NCH, int G>
-__global__ void __launch_bounds__(64, ((NCH > 0 && G == 1) || NCH < 0) ? 4 : 2) ngt_graph_search_kernel(SearchArgs a) {
+__global__ void __launch_bounds__(64, (search_waves_per_simd<M, NCH, G>())) ngt_graph_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = lane_id();
   SearchState st;
