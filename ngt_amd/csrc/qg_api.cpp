@@ -389,8 +389,6 @@ extern "C" int ngt_amd_qg_search_device(ngt_amd_index* ix, const ngt_amd_qg_sear
   a.recs = q.packed ? q.recs.p : nullptr;
   a.qkw = q.qkw.p;
   a.rec_shift = q.rec_shift;
-  a.rec_pf = 0u;
-  if (const char* v = ngt_amd::knob("NGT_AMD_QG_PF")) a.rec_pf = atoi(v) != 0 ? 1u : 0u;
   a.queries = static_cast<const uint8_t*>(d_queries);
   a.query_bytes = query_bytes;
   a.nq = nq;

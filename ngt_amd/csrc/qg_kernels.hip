@@ -710,8 +710,7 @@ __device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, co
                                                        uint32_t Me, float scale, float toff, uint32_t* nid,
                                                        uint32_t* nkw, float* dists, bool probe, const SearchState& st,
                                                        const uint8_t* vis, uint32_t epoch, float expr,
-                                                       uint64_t (&seen)[2], const uint8_t* pf, uint32_t pfl,
-                                                       uint8_t* pfbuf) {
+                                                       uint64_t (&seen)[2]) {
   const int lane = lane_id();
   const uint32_t npairs = Me >> 1;
   const uint64_t blk = (uint64_t)8 * Me;
@@ -744,13 +743,6 @@ __device__ __forceinline__ uint32_t ids_and_adc_packed(const LaneLut<PPL>& L, co
       nkw[j + lane] = e.y;
     }
     deg += (uint32_t)__popcll(ballot64(e.x != 0u));
-  }
-  // the next key's record towards L2 (one dword per 128-B line, LDS-DMA into
-  // a scratch line: no register waits on it), issued behind this record's
-  // loads so the waits above do not include it
-  if ((uint32_t)lane < pfl) {
-    typedef __attribute__((address_space(3))) void* lds_ptr;
-    __builtin_amdgcn_global_load_lds((const void*)(pf + (uint64_t)lane * 128u), (lds_ptr)pfbuf, 4, 0, 0);
   }
   const uint32_t nbd = deg == 0 ? 0 : (deg - 1) / 16 + 1;
   // lane l's entries' ADC distances (entry 64 * cc + l)
@@ -915,8 +907,6 @@ __global__ void __launch_bounds__(64, NGT_AMD_QG_WPE) ngt_qg_search_kernel(QgSea
   p += (size_t)4 * nstage64;
   uint32_t* hist = reinterpret_cast<uint32_t*>(p);  // threshold selection: 64 counters, then 64 staged keys
   p += 256 + 512;
-  uint8_t* pfbuf = p;  // the record prefetch's LDS-DMA sink (never read)
-  p += 256;
   float* qlds = reinterpret_cast<float*>(p);
   const bool packed = a.recs != nullptr;
 
@@ -1188,23 +1178,9 @@ __global__ void __launch_bounds__(64, NGT_AMD_QG_WPE) ngt_qg_search_kernel(QgSea
       if (packed) {
         // the key word names the record and its block count (qg_api.cpp qg_pack)
         const uint8_t* rec = a.recs + ((uint64_t)(target >> 3) << a.rec_shift);
-        // the next pop unless this expansion accepts a closer key: the
-        // head's first key after this pop
-        const uint8_t* pf = nullptr;
-        uint32_t pfl = 0u;
-        if (a.rec_pf && hn != 0u) {
-          const uint64_t nk = readlane_u64(hk, 0);
-          if (key_dist(nk) <= expr) {
-            const uint32_t kw = key_id(nk);
-            pf = a.recs + ((uint64_t)(kw >> 3) << a.rec_shift);
-            const uint32_t bytes = ((kw & 7u) + 1u) * (8u * a.Me + 128u);
-            pfl = (bytes + 127u) / 128u;
-            if (pfl > 64u) pfl = 64u;
-          }
-        }
         deg = ids_and_adc_packed<PPL, (NB > 0 ? NB : 1)>(L, rec, (target & 7u) + 1u, a.Me, scale, toff, st.nid, nkw,
                                                          st.nd, !use_hash && st.vf != nullptr, st, vis, epoch,
-                                                         expr, seen_pre, pf, pfl, pfbuf);
+                                                         expr, seen_pre);
         NGT_MARK(t_ids);
       } else if (early) {
         deg = ids_and_adc<PPL, (NB > 0 ? NB : 1)>(L, nbr, a.id_stride, a.qcodes + (uint64_t)target * a.code_stride,
@@ -1390,7 +1366,7 @@ size_t qg_search_lds_bytes(const QgSearchArgs& a) {
   b += 2 * (((size_t)8 * (a.size + 1) + 15) & ~(size_t)15);
   const uint32_t nstage = a.id_stride > a.size ? a.id_stride : a.size;
   b += (size_t)12 * ((nstage + 63) & ~63u);
-  b += 256 + 512 + 256;  // threshold-selection counters and staged keys, the prefetch sink
+  b += 256 + 512;  // threshold-selection counters and staged keys
   b += (size_t)a.dp * 4;
   return b;
 }
