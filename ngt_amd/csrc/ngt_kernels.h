@@ -489,7 +489,6 @@ struct QgSearchArgs {
   const uint8_t* recs;           // packed records (QgState::recs), or null: the fixed-stride slabs
   const uint32_t* qkw;           // [nrows] key words of the packed layout
   uint32_t rec_shift;            // record unit = 1 << rec_shift bytes
-  uint32_t rec_pf;               // packed layout: read the next key's record towards L2 under each expansion
   uint32_t* out_ids;             // [nq][k]
   float* out_dists;
   uint32_t* out_n;
