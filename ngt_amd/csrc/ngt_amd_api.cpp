@@ -593,8 +593,13 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
     // saturate any LDS-sized filter: epochs alone there.
     a.ht_log2 = 0;
     // 512 unchecked keys in LDS (exact HBM spill beyond): C3's long rows then
-    // fit 16 waves per CU instead of 11 (+6 % QPS)
+    // fit 16 waves per CU instead of 11 (+6 % QPS).  Long cosine/angle rows
+    // run at 12 waves per CU (search_kernels.hip), whose LDS holds 768: 794
+    // vs 808 ms per C3 launch (profiles/r5zk)
     a.cq_cap = 512;
+    if (ix->row_bytes > 1024 && ix->otype == NGT_AMD_OBJECT_FLOAT &&
+        (ix->metric == NGT_AMD_DISTANCE_COSINE || ix->metric == NGT_AMD_DISTANCE_ANGLE))
+      a.cq_cap = 768;
     if (ix->row_bytes <= 1024) {
       a.vf_log2 = 15;
       // -2: the filter and epochs hold accepted ids only (a few thousand per
