@@ -315,9 +315,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--mode", choices=["exact", "qg", "shard", "capi"], default="exact")
-    ap.add_argument("--threads", type=int, default=64,
-                    help="C-API lines: concurrent callers T (runs at 1, T and 2T threads; the serving grid has 128 "
-                         "workers)")
+    ap.add_argument("--threads", type=int, default=128,
+                    help="C-API lines: concurrent callers T (runs at 1, T and 2T threads; the serving grid has one "
+                         "worker per CU but one)")
     ap.add_argument("--qg", action="store_true", help="with --mode shard: NGTQG shards (C5's form)")
     ap.add_argument("--config", choices=["c2", "c3"], default="c2")
     ap.add_argument("--n", type=int, default=0, help="objects (per shard in --mode shard)")
@@ -353,7 +353,14 @@ def main():
     ap.add_argument("--max-deg", type=int, default=256)
     ap.add_argument("--seed-size", type=int, default=10)
     ap.add_argument("--eps", type=str, default="")
-    ap.add_argument("--expansion", type=float, default=3.0, help="NGTQG result_expansion")
+    ap.add_argument("--expansion", type=float, default=3.0,
+                    help="NGTQG result_expansion (ngtqg_search's default 3.0, NGTQ/Capi.cpp:44)")
+    ap.add_argument("--qg-expansions", type=str, default="",
+                    help="--mode qg: result_expansion candidates; epsilon is tuned to the target for each and the "
+                         "one whose full-batch launch is shortest is timed")
+    ap.add_argument("--qg-line", choices=["auto", "on", "off"], default="auto",
+                    help="attach NGTQG (ngtqg quantize on the device) over the same saved 1M ANNG as the 'qg' key "
+                         "(a child run of --mode qg --graph anng); auto = on for the default single-GPU C2 run")
     ap.add_argument("--qg-edges", type=int, default=128, help="NGTQG max edges per node")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sweep-nq", type=int, default=2000, help="queries per epsilon-sweep launch")
@@ -453,8 +460,8 @@ def main():
     anng_check = None
     capi_dir = None
     capi_tmp = False
-    if (args.graph == "anng" and world == 1 and not args.pmc_launches and N == 1_000_000 and D == 128
-            and args.anng_batch == 200 and (args.capi_line == "on" or args.capi_line == "auto")):
+    if (args.graph == "anng" and args.mode == "exact" and world == 1 and not args.pmc_launches and N == 1_000_000
+            and D == 128 and args.anng_batch == 200 and (args.capi_line == "on" or args.capi_line == "auto")):
         # the C-API line opens the index this run saves (ngt_save_index) from disk
         import tempfile
         if not args.anng_dir:
@@ -599,14 +606,40 @@ def main():
         log("eps %.4f recall@%d %.4f kernel %.2f ms (%d queries)" % (eps, K, r, sweep[-1][2], nq))
         return r
 
-    chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None,
-                          last_ms=lambda: sweep[-1][2] * NQ / max(1, sweep[-1][3]))
-    rec = measure(chosen, NQ)
-    for _ in range(20):
-        if rec >= args.target or args.eps:
-            break
-        chosen = round(chosen * 1.02 + 1e-4, 5)
+    def tune():
+        eps = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None,
+                           last_ms=lambda: sweep[-1][2] * NQ / max(1, sweep[-1][3]))
+        r = measure(eps, NQ)
+        for _ in range(20):
+            if r >= args.target or args.eps:
+                break
+            eps = round(eps * 1.02 + 1e-4, 5)
+            r = measure(eps, NQ)
+        return eps, r
+
+    expansion_sweep = None
+    if qgm and args.qg_expansions and not args.eps:
+        # NGTQG's two knobs: for every result_expansion candidate the smallest
+        # epsilon reaching the target, then the one whose whole-batch launch
+        # (the last measurement of its tuning) is shortest
+        expansion_sweep = []
+        for ex in [float(x) for x in args.qg_expansions.split(",")]:
+            args.expansion = ex
+            eps_x, rec_x = tune()
+            expansion_sweep.append({"result_expansion": ex, "epsilon": eps_x, "recall_at_10": rec_x,
+                                    "kernel_ms": sweep[-1][2]})
+            log("result_expansion %g: epsilon %.5f recall@%d %.4f, %.2f ms per %d-query launch" % (
+                ex, eps_x, K, rec_x, sweep[-1][2], NQ))
+        ok = [e for e in expansion_sweep if e["recall_at_10"] >= args.target] or expansion_sweep
+        fastest = min(e["kernel_ms"] for e in ok)
+        # launches within 3 % of the fastest are a tie (run-to-run noise): the
+        # one nearest the C API's default 3.0 is taken, so the pick repeats
+        best = min([e for e in ok if e["kernel_ms"] <= fastest * 1.03],
+                   key=lambda e: (abs(e["result_expansion"] - 3.0), e["result_expansion"]))
+        args.expansion, chosen = best["result_expansion"], best["epsilon"]
         rec = measure(chosen, NQ)
+    else:
+        chosen, rec = tune()
     if dist is not None and not shard:
         # replicas: all ranks use the largest epsilon any rank needed
         t = torch.tensor([chosen], device=dev)
@@ -920,6 +953,13 @@ def main():
                          "effective_gbs_literal": literal / (kernel_ms * 1e-3) / 1e9,
                          "effective_frac_literal": literal / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                          "infinity_cache_resident_share": ic_share(split, alg_bytes),
+                         # the bytes from tables larger than the 256 MiB Infinity Cache (f32 rows,
+                         # adjacency, quantized-graph records, visited epochs, queries, results): what
+                         # has to come from HBM itself, over the same kernel time
+                         "hbm_side_bytes_per_launch": alg_bytes * (1.0 - ic_share(split, alg_bytes)),
+                         "hbm_side_gbs": alg_bytes * (1.0 - ic_share(split, alg_bytes)) / (kernel_ms * 1e-3) / 1e9,
+                         "hbm_side_frac": (alg_bytes * (1.0 - ic_share(split, alg_bytes)) / (kernel_ms * 1e-3) / 1e9
+                                           / PEAK_HBM_GBS),
                          # the same bytes over the whole step with launches overlapping on the streams
                          # (a single launch's last round of queries leaves the GPU part-empty)
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
@@ -970,12 +1010,17 @@ def main():
                     "SQ_INSTS_LDS": cn.get("SQ_INSTS_LDS"),
                     "trace_avg_kernel_ms": tentry.get("trace_avg_kernel_ms")})
                 # what bounds the kernel, from the wave-cycle partition
-                line["roofline"]["bound"] = bound_from_counters(cn)
+                line["roofline"]["bound"] = bound_from_counters(cn, ic_share(split, alg_bytes))
                 line["roofline"]["bound_note"] = (
-                    "from the SQ wave-cycle partition (wait_any_frac >= 0.5: dependent gathers, not HBM "
-                    "bandwidth); achieved/peak still against the 8 TB/s HBM figure")
+                    "from the SQ wave-cycle partition and the byte split: 'latency' when >= 0.5 of the "
+                    "wave-cycles are parked on s_waitcnt (dependent gathers), 'valu' when VALU issues on "
+                    ">= 0.5, 'infinity-cache' when most algorithmic bytes come from a table the 256 MiB "
+                    "Infinity Cache holds, else 'hbm'; achieved/frac are against the 8 TB/s HBM figure, "
+                    "hbm_side_frac counts only the bytes from tables beyond the Infinity Cache")
         if qgm:
             line["config"]["result_expansion"] = args.expansion
+            if expansion_sweep is not None:
+                line["config"]["result_expansion_sweep"] = expansion_sweep
             line["config"]["qg_layout"] = (
                 {"packed_record_bytes": qg_record_bytes, "bytes_per_node": qg_record_bytes / N,
                  "what": "per node ceil(deg/16) code blocks of 8*Me bytes + 16 {id, key word} entries per block "
@@ -990,12 +1035,24 @@ def main():
                 line["config"]["exact_neighbour_distances_per_query"] = float(c[:, 6].mean())
             if evals_per_query is not None:
                 line["config"]["evaluations_per_query"] = evals_per_query
-        want_anng = args.anng_line == "on" or (args.anng_line == "auto" and args.mode == "exact" and not c3
-                                               and args.graph == "knn" and world == 1)
-        if want_anng:
-            line["anng"] = anng_child_line(args)
-        want_c3 = args.c3_line == "on" or (args.c3_line == "auto" and args.mode == "exact" and not c3
-                                           and args.graph == "knn" and world == 1 and N == 1_000_000
+        headline_run = args.mode == "exact" and not c3 and args.graph == "knn" and world == 1
+        want_anng = args.anng_line == "on" or (args.anng_line == "auto" and headline_run)
+        want_qg = args.qg_line == "on" or (args.qg_line == "auto" and headline_run and N == 1_000_000
+                                           and not args.pmc_launches)
+        if want_anng or want_qg:
+            # the ANNG line builds and saves the 1M ANNG here; the QG line
+            # quantizes that same index
+            import shutil
+            import tempfile
+            index_dir = tempfile.mkdtemp(prefix="ngt_anng_")
+            try:
+                if want_anng:
+                    line["anng"] = anng_child_line(args, index_dir)
+                if want_qg:
+                    line["qg"] = qg_child_line(args, index_dir)
+            finally:
+                shutil.rmtree(index_dir, ignore_errors=True)
+        want_c3 = args.c3_line == "on" or (args.c3_line == "auto" and headline_run and N == 1_000_000
                                            and not args.pmc_launches)
         if want_c3:
             line["c3"] = c3_child_line(args)
@@ -1051,77 +1108,133 @@ def ic_share(split, alg_bytes):
     return float(split["filter_copy_bytes"] / alg_bytes)
 
 
-def bound_from_counters(cn):
+def bound_from_counters(cn, ic_resident_share=0.0):
     """What bounds the kernel, from the SQ wave-cycle partition
     (MI355X_MICROARCH.md rocprofv3 PMC): more than half the wave-cycles parked
     on s_waitcnt = dependent-gather latency; else VALU-issue bound if VALU
-    issues on more than half; else the memory system."""
+    issues on more than half; else the memory system -- the Infinity Cache
+    when most of the algorithmic bytes come from a table it holds (the C2
+    filter copy), HBM otherwise."""
     w = cn["SQ_WAVE_CYCLES"]
     if cn.get("SQ_WAIT_ANY", 0) / w >= 0.5:
         return "latency"
     if cn.get("SQ_ACTIVE_INST_VALU", 0) / w >= 0.5:
         return "valu"
+    if ic_resident_share >= 0.5:
+        return "infinity-cache"
     return "hbm"
 
 
-def anng_child_line(args):
-    """The index a `ngt create` user has, measured beside the headline: the
-    1M ANNG (E 10) built on the device through the C API (files identical to
-    the reference's build), searched at the prf's EdgeSizeForSearch 40
-    (Command.cpp:39, Graph.h:675-692) from DVP-tree seeds.  A child process
-    of this bench (`--graph anng`), so its line carries its own roofline,
-    cpu_baseline, parity sample and reference checks; None if it fails."""
+def group_members(pgid):
+    """Pids of live processes in process group pgid (from /proc)."""
+    pids = []
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open("/proc/%s/stat" % d) as f:
+                st = f.read()
+        except OSError:
+            continue
+        fields = st[st.rfind(")") + 2:].split()
+        if len(fields) > 2 and fields[0] != "Z" and int(fields[2]) == pgid:
+            pids.append(int(d))
+    return pids
+
+
+def run_reaped(argv, timeout, env=None, capture_stderr=False, what="child"):
+    """Run a child command in its own session (process group) and wait for it;
+    afterwards anything it left behind in that group is terminated, so no
+    process of this bench outlives it.  Returns (returncode, stdout, stderr)."""
+    import signal
     import subprocess
-    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--graph", "anng", "--anng-line", "off",
-           "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1", "--cpu-seconds", str(min(args.cpu_seconds, 8.0)),
-           "--latency-queries", "20"]
+    import threading
+    p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE if capture_stderr else None, env=env,
+                         start_new_session=True)
+    # the pipes are drained by threads and the wait is for the child itself:
+    # a leftover holding the pipes open must not keep this call waiting
+    got = {}
+    readers = [threading.Thread(target=lambda n, f: got.__setitem__(n, f.read()), args=(n, f), daemon=True)
+               for n, f in (("out", p.stdout), ("err", p.stderr)) if f is not None]
+    for t in readers:
+        t.start()
+    try:
+        p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        log("%s: no exit after %d s; stopping its process group" % (what, timeout))
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+    left = group_members(p.pid)
+    if left:
+        log("%s left %d process(es) behind (%s); terminating them" % (what, len(left), left))
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+            for _ in range(50):
+                if not group_members(p.pid):
+                    break
+                time.sleep(0.1)
+            if group_members(p.pid):
+                os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+    for t in readers:
+        t.join(10)
+    return (p.returncode, (got.get("out") or b"").decode(errors="replace"),
+            (got.get("err") or b"").decode(errors="replace"))
+
+
+def child_line(args, name, extra, cpu_seconds, latency_queries):
+    """One of the lines measured beside the headline: a child process of this
+    bench with its own roofline, cpu_baseline and parity sample (its JSON line
+    without the sweep), or {"error": ...} if it fails."""
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + extra + [
+        "--anng-line", "off", "--c3-line", "off", "--qg-line", "off",
+        "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1",
+        "--cpu-seconds", str(min(args.cpu_seconds, cpu_seconds)), "--latency-queries", str(latency_queries)]
     if args.no_cpu:
         cmd.append("--no-cpu")
     t0 = time.time()
-    log("ANNG line: %s" % " ".join(cmd[2:]))
+    log("%s line: %s" % (name, " ".join(cmd[2:])))
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=env, timeout=900)
-    out = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
-    if r.returncode != 0 or not out:
-        log("ANNG line failed (rc %d)" % r.returncode)
-        return {"error": "child run failed", "rc": r.returncode}
+    rc, stdout, _ = run_reaped(cmd, 900, env=env, what="%s line" % name)
+    out = [l for l in stdout.splitlines() if l.startswith("{")]
+    if rc != 0 or not out:
+        log("%s line failed (rc %d)" % (name, rc))
+        return {"error": "child run failed", "rc": rc}
     d = json.loads(out[-1])
     d.pop("sweep", None)
     d["child_wall_s"] = time.time() - t0
-    log("ANNG line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
-        d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
+    log("%s line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
+        name, d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
     return d
+
+
+def anng_child_line(args, index_dir):
+    """The index a `ngt create` user has, measured beside the headline: the
+    1M ANNG (E 10) built on the device through the C API (files identical to
+    the reference's build, saved to index_dir), searched at the prf's
+    EdgeSizeForSearch 40 (Command.cpp:39, Graph.h:675-692) from DVP-tree
+    seeds; with its `capi` sub-key (the drop-in C API on the saved index)."""
+    return child_line(args, "ANNG", ["--graph", "anng", "--anng-dir", index_dir], 8.0, 20)
+
+
+def qg_child_line(args, index_dir):
+    """BASELINE config 5's path on one GPU: `ngtqg quantize` on the device
+    (kmeansWithNGT codebooks, encoder, quantized graph of <= 128 edges;
+    QuantizedGraph.h:456-475) over the 1M ANNG the ANNG line saved (opened
+    with ngt_open_index; rebuilt if that line failed), searched with
+    NGTQG::Index::search from DVP-tree seeds (QuantizedGraph.h:354-372) at the
+    result_expansion / epsilon pair that reaches recall@10 0.95 fastest."""
+    return child_line(args, "QG", ["--mode", "qg", "--graph", "anng", "--anng-dir", index_dir,
+                                   "--qg-expansions", "2,3,4,6"], 10.0, 0)
 
 
 def c3_child_line(args):
     """C3 (BASELINE config 3: 1M x 960 float cosine, kNN graph, the cosine
-    filter) measured beside the headline: a child process of this bench
-    (`--config c3`) with its own roofline, cpu_baseline and parity sample;
-    None if it fails."""
-    import subprocess
-    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", "c3", "--anng-line", "off", "--c3-line", "off",
-           "--steps", str(max(3, min(args.steps, 5))), "--warmup", "1", "--cpu-seconds", str(min(args.cpu_seconds, 10.0)),
-           "--latency-queries", "0"]
-    if args.no_cpu:
-        cmd.append("--no-cpu")
-    t0 = time.time()
-    log("C3 line: %s" % " ".join(cmd[2:]))
-    env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
-        env.pop(k, None)
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=env, timeout=900)
-    out = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
-    if r.returncode != 0 or not out:
-        log("C3 line failed (rc %d)" % r.returncode)
-        return {"error": "child run failed", "rc": r.returncode}
-    d = json.loads(out[-1])
-    d.pop("sweep", None)
-    d["child_wall_s"] = time.time() - t0
-    log("C3 line: %.0f QPS at recall %.4f, frac %.3f (%.0f s)" % (
-        d["value"], d["config"]["recall_at_10"], d["roofline"]["frac"], d["child_wall_s"]))
-    return d
+    filter) measured beside the headline."""
+    return child_line(args, "C3", ["--config", "c3"], 10.0, 0)
 
 
 def capi_anng_line(index_dir, Q, gt, D, K, eps, threads):
@@ -1723,10 +1836,6 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm, emi
             "cpu_baseline": cpu, "parity_sample": parity, "sweep": sweep}
         if qgm:
             line["config"]["result_expansion"] = args.expansion
-        want_anng = args.anng_line == "on" or (args.anng_line == "auto" and args.mode == "exact" and not c3
-                                               and args.graph == "knn" and world == 1)
-        if want_anng:
-            line["anng"] = anng_child_line(args)
         if not emit:
             return line
         print(json.dumps(line), file=result_out, flush=True)
@@ -1815,7 +1924,8 @@ def shard_parity_sample(args, shards, qdev, seeds, eps, merged, qgm, dist=None):
     cpu = {"value": n / el_max, "unit": "queries/s", "cores": cores, "kind": "port",
            "sample": "first %d queries over all %d shards, oracle/ngt_oracle.c %s built -O3 -march=x86-64-%s, "
                      "one query per thread per shard on %d threads per rank x %d ranks, %.1f s (max over ranks); "
-                     "host: %s, %d CPUs" % (n, nsh, what, isa, threads, world, el_max, model, ncpu)}
+                     "host: %s, %d CPUs" % (n, nsh, what, isa, threads, world, el_max, model, ncpu),
+           "all_physical_cores": all_cores_note(n / el_max, cores)}
     return cpu, parity
 
 
@@ -1826,23 +1936,25 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads, plan=None, keep_ids=Fals
     The calls are answered by the resident serving grid (serve.cpp; its grid
     launches and answered calls are in each run's `launches` / `served`);
     requests it does not take fall back to group-committed launches."""
-    import subprocess
     exe = os.path.join(index_dir, "capi_threads")
-    subprocess.check_call(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-o", exe,
-                           os.path.join(ROOT, "tests", "cxx", "capi_threads.c"), "-L", os.path.join(ROOT, "ngt_amd"),
-                           "-lngt_amd", "-Wl,-rpath," + os.path.join(ROOT, "ngt_amd"), "-lpthread", "-lm"])
+    rc, _, err = run_reaped(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-o", exe,
+                             os.path.join(ROOT, "tests", "cxx", "capi_threads.c"), "-L", os.path.join(ROOT, "ngt_amd"),
+                             "-lngt_amd", "-Wl,-rpath," + os.path.join(ROOT, "ngt_amd"), "-lpthread", "-lm"], 120,
+                            capture_stderr=True, what="gcc capi_threads.c")
+    if rc != 0:
+        raise SystemExit("bench: capi_threads.c did not compile: %s" % err[-2000:])
     qpath = os.path.join(index_dir, "queries.f32")
     np.ascontiguousarray(Q, np.float32).tofile(qpath)
     out = []
     for t, calls in plan or [(1, 300), (threads, 200), (2 * threads, 150)]:
         ids_path = os.path.join(index_dir, "ids.u32")
-        env = dict(os.environ)
-        r = subprocess.run([exe, index_dir, qpath, str(Q.shape[0]), str(D), str(K), repr(float(eps)), str(t),
-                            str(calls), ids_path], env=env, capture_output=True, text=True, timeout=600)
-        if r.returncode != 0:
-            raise SystemExit("bench: capi_threads failed: %s" % r.stderr[-2000:])
-        res = json.loads(r.stdout.strip().splitlines()[-1])
-        for ln in [x for x in r.stderr.splitlines() if x.startswith("[serve]")][:20]:
+        rc, stdout, err = run_reaped([exe, index_dir, qpath, str(Q.shape[0]), str(D), str(K), repr(float(eps)), str(t),
+                                      str(calls), ids_path], 600, env=dict(os.environ), capture_stderr=True,
+                                     what="C client (%d threads)" % t)
+        if rc != 0:
+            raise SystemExit("bench: capi_threads failed: %s" % err[-2000:])
+        res = json.loads(stdout.strip().splitlines()[-1])
+        for ln in [x for x in err.splitlines() if x.startswith("[serve]")][:20]:
             log("C client %d threads: %s" % (t, ln))
         ids = np.fromfile(ids_path, np.uint32).reshape(-1, K).astype(np.int64)
         qi = np.arange(ids.shape[0]) % Q.shape[0]
@@ -1854,6 +1966,35 @@ def capi_c_client(index_dir, Q, gt, D, K, eps, threads, plan=None, keep_ids=Fals
             t, res["qps"], res["latency_ms"]["mean"], res["latency_ms"]["p99"], res["recall_at_10"],
             res.get("launches", -1)))
     return out
+
+
+def physical_cores():
+    """Physical cores of the host (lscpu: cores per socket x sockets), or None."""
+    try:
+        import subprocess
+        per, sockets = None, None
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            if line.startswith("Core(s) per socket:"):
+                per = int(line.split(":", 1)[1])
+            elif line.startswith("Socket(s):"):
+                sockets = int(line.split(":", 1)[1])
+        return per * sockets if per and sockets else None
+    except (OSError, ValueError):
+        return None
+
+
+def all_cores_note(value, threads):
+    """The CPU baseline scaled linearly to every physical core of the host (one
+    query per thread, nothing shared: the best case for the CPU) -- the GPU/CPU
+    ratio against the whole host is the reported ratio x threads / cores."""
+    cores = physical_cores()
+    if not cores:
+        return None
+    return {"physical_cores": cores, "value_at_all_physical_cores_linear": value * cores / threads,
+            "ratio_factor": threads / float(cores),
+            "note": "measured on %d threads (the lease's CPU affinity); at all %d physical cores, scaled linearly, "
+                    "the CPU would reach %.0f queries/s, so every GPU/CPU ratio against this baseline shrinks by "
+                    "x%.3f" % (threads, cores, value * cores / threads, threads / float(cores))}
 
 
 def host_cpu():
@@ -2011,9 +2152,43 @@ def cpu_baseline(args, ix, rows, offsets, edges, qdev, seeds, eps, metric, gpu_o
             "reference_equivalent_value": (done / el / cal["ratio_port_over_reference_1thread"]) if cal else None,
             "sample": "first %d of the %d queries (same graph, seeds, epsilon), oracle/ngt_oracle.c %s built -O3 "
                       "-march=x86-64-%s (16-lane FMA order kept), one query per thread on %d threads, %.1f s; "
-                      "host: %s, %d CPUs" % (done, nq, what, isa, threads, el, model, ncpu)}
+                      "host: %s, %d CPUs" % (done, nq, what, isa, threads, el, model, ncpu),
+            "all_physical_cores": all_cores_note(done / el, threads)}
     return base, parity
 
 
+def reap_children():
+    """Before exiting: any child process of this bench still alive (there
+    should be none -- every child runs through run_reaped) is named on stderr
+    and terminated, so nothing outlives the run."""
+    import signal
+    me = os.getpid()
+    left = []
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open("/proc/%s/stat" % d) as f:
+                st = f.read()
+        except OSError:
+            continue
+        fields = st[st.rfind(")") + 2:].split()
+        if len(fields) > 1 and fields[0] != "Z" and int(fields[1]) == me:
+            left.append(int(d))
+    for pid in left:
+        try:
+            with open("/proc/%d/cmdline" % pid, "rb") as f:
+                cmd = f.read().replace(b"\0", b" ").decode(errors="replace").strip()
+        except OSError:
+            cmd = "?"
+        print("[bench] child %d still running at exit (%s); terminating it" % (pid, cmd), file=sys.stderr, flush=True)
+        try:
+            os.kill(pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+
+
 if __name__ == "__main__":
-    sys.exit(main() or 0)
+    rc = main() or 0
+    reap_children()
+    sys.exit(rc)

@@ -234,7 +234,9 @@ class Index(object):
         h = self._L.ngt_get_device_index(self.index, self.err)
         if not h:
             raise NativeError(_err_string(self._L, self.err))
-        return DeviceIndex.wrap(h, int(self.distance_type), "float" if self.is_float else "uint8", self.dim)
+        # nrows: the repository's slots, dummy slot 0 included (the device rows)
+        return DeviceIndex.wrap(h, int(self.distance_type), "float" if self.is_float else "uint8", self.dim,
+                                nrows=int(self._L.ngt_get_object_repository_size(self.index, self.err)))
 
     def save(self, path=None):
         if path is None:

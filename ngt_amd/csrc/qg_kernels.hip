@@ -959,7 +959,28 @@ __global__ void __launch_bounds__(64, NGT_AMD_QG_WPE) ngt_qg_search_kernel(QgSea
     uint64_t hk = ~0ull, B = ~0ull, T = ~0ull;
     uint32_t hn = 0, ntail = 0, nspill = 0;
     uint64_t* tail = st.cq;
+    uint32_t ntrim = 0;  // spill trims (counter 7)
+    // a full spill first drops its keys beyond the exploration radius (they
+    // can never be popped: expr only shrinks); the capacity error is left for
+    // a spill still full of keys within it
+    auto spill_trim = [&]() {
+      const uint64_t lim = ((uint64_t)ord_of(expr) << 32) | 0xffffffffull;
+      uint32_t out = 0;
+      for (uint32_t b0 = 0; b0 < nspill; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const uint64_t key = i < nspill ? spill[i] : ~0ull;
+        const bool kp = i < nspill && key <= lim;
+        const uint64_t km = ballot64(kp);
+        __builtin_amdgcn_wave_barrier();
+        if (kp) spill[out + mbcnt(km)] = key;
+        __builtin_amdgcn_wave_barrier();
+        out += (uint32_t)__popcll(km);
+      }
+      nspill = out;
+      ntrim++;
+    };
     auto spill_push = [&](uint64_t key) {
+      if (nspill >= a.spill_cap) spill_trim();
       if (nspill >= a.spill_cap) {
         if (lane == 0) atomicOr(a.error, 1);
       } else {
@@ -991,6 +1012,7 @@ __global__ void __launch_bounds__(64, NGT_AMD_QG_WPE) ngt_qg_search_kernel(QgSea
         const bool kp = i < ntail && key < l;
         const uint64_t mm = ballot64(mv), km = ballot64(kp);
         const uint32_t nm = (uint32_t)__popcll(mm);
+        if (nspill + nm > a.spill_cap) spill_trim();
         if (nspill + nm > a.spill_cap) {
           if (lane == 0) atomicOr(a.error, 1);
         } else if (mv) {
@@ -1290,7 +1312,7 @@ __global__ void __launch_bounds__(64, NGT_AMD_QG_WPE) ngt_qg_search_kernel(QgSea
         c[4] = nblk;
         c[5] = maxq;
         c[6] = (bitmap_mode && use_hash) ? 1 : 0;
-        c[7] = 0;
+        c[7] = ntrim;
 #ifdef NGT_AMD_STAMPS
         c[4] = t_pop;
         c[5] = t_ids;

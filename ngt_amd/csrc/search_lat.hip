@@ -105,7 +105,7 @@ __device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
 }
 
 // ---- serving form (ngt_kernels.h ServeArgs) ---------------------------------
-// The dispatcher (one lane of the extra block): publishes each ticket whose
+// The dispatcher (one lane of block 0): publishes each ticket whose
 // request slot the host has posted, in ticket order, until the host asks it
 // to stop, nothing was posted for idle_ticks, or life_ticks have passed;
 // then tells the workers to drain.
@@ -231,7 +231,9 @@ template <int NCH, int W, bool SERVE>
 __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs a, ServeArgs sv) {
   constexpr int EG = 2;
   if constexpr (SERVE) {
-    if (blockIdx.x == sv.workers) {
+    // the dispatcher is block 0, so it is placed first even when the grid
+    // (one workgroup per CU) has more blocks than free CUs
+    if (blockIdx.x == 0) {
       if (threadIdx.x < 64) serve_dispatch(sv);
       return;
     }
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
   constexpr uint32_t NT = 64u * W;
   const uint32_t bm_words = (a.nrows + 31u) / 32u;
   const uint32_t nslots = a.lat_slots;  // speculation slots, issued by the commit wave
-  const uint32_t wg = blockIdx.x;
+  const uint32_t wg = SERVE ? blockIdx.x - 1u : blockIdx.x;  // serving: workers are blocks 1..workers
   uint64_t* spill = a.spill + (uint64_t)wg * a.spill_cap;
   const int g = lane & 3, rs = lane >> 2;
 
@@ -302,6 +304,9 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       }
       if (tid == 0) {
         ctl->done = 0u;
+        // no hop prefetch before this query's first set_expr (the speculation
+        // waves read it atomically; +inf would let a stale query's radius in)
+        __hip_atomic_store(&ctl->expr, -1.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ctl->sp[0] = ctl->sp[1] = ctl->sp[2] = ctl->sp[3] = 0ull;
         if constexpr (SERVE) {
           const ServeReqHdr* h = reinterpret_cast<const ServeReqHdr*>(req);
@@ -350,7 +355,7 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       float expr = 0.f;
       auto set_expr = [&]() {
         expr = __fmul_rn(coefq, radius);
-        if (lane == 0) ctl->expr = expr;
+        if (lane == 0) __hip_atomic_store(&ctl->expr, expr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       };
       // unchecked set: head (registers, sorted, hn keys) < B <= tail (LDS,
       // ntail keys) < T <= spill (HBM, nspill keys)
@@ -618,8 +623,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
-          // the state's release publishes the claim word with the rest
-          __hip_atomic_store(&slots[s].claim, gen << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          // released on its own as well: a speculation wave that CASes this
+          // word (having read the slot's previous kIssued state) acquires
+          // the key written above through it
+          __hip_atomic_store(&slots[s].claim, gen << 8, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           lds_store_rel(&slots[s].state, kIssued);
         }
         return s;

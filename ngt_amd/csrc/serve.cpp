@@ -22,7 +22,7 @@
 // commit wave), so results equal the reference's.
 //
 //   NGT_AMD_SERVE=0             never serve (callers take the launch path)
-//   NGT_AMD_SERVE_WORKERS=n     worker workgroups, one query each (default 128)
+//   NGT_AMD_SERVE_WORKERS=n     worker workgroups, one query each (default: CUs - 1)
 //   NGT_AMD_SERVE_IDLE_MS=n     idle time before the grid leaves (default 20)
 //   NGT_AMD_SERVE_LOG=1         a stderr line per grid: lifetime, why it left
 #include <float.h>
@@ -88,7 +88,7 @@ struct Server {
   DevBuf<ServeDevCtl> dctl;
   DevBuf<uint64_t> spill;
   DevBuf<int> err;
-  uint32_t workers = 128;
+  uint32_t workers = 0;  // server_init: CUs - 1
   uint64_t clock_khz = 100000;
   double idle_ms = 20.0, life_s = 10.0;
   // tickets
@@ -135,8 +135,9 @@ int server_init(ngt_amd_index* ix, Server* sv) {
   HIP_OK(sv->err.alloc(1));
   HIP_OK(hipMemsetAsync(sv->err.p, 0, sizeof(int), sv->s));
   HIP_OK(hipStreamSynchronize(sv->s));
+  // one worker per CU but the dispatcher's (each workgroup owns its CU's LDS)
   const char* v = ngt_amd::knob("NGT_AMD_SERVE_WORKERS");
-  const int w = v ? atoi(v) : 128;
+  const int w = v ? atoi(v) : ix->cu_count - 1;
   sv->workers = (uint32_t)std::max(1, std::min(w, ix->cu_count - 1));
   if (const char* t = ngt_amd::knob("NGT_AMD_SERVE_IDLE_MS")) sv->idle_ms = std::max(1.0, atof(t));
   if (const char* t = ngt_amd::knob("NGT_AMD_SERVE_LOG")) sv->log = atoi(t) != 0;

@@ -326,6 +326,8 @@ class DeviceIndex(object):
 
     def qg_get_graph(self):
         """(ids [nrows, max_degree] 0-terminated, codes [nrows, code_stride])."""
+        if self.nrows <= 0:
+            raise NativeError("qg_get_graph: the view does not know the index's row count")
         md = self.qg_max_degree()
         cs = int(self.L.ngt_amd_qg_code_stride(self.h))
         ids = np.zeros((self.nrows, md), np.uint32)

@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 6 b: the spill-trim test alone (its outcome table), then the rest of
+# gpu_r6a
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r6b}; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread \
+  tests/test_gpu_qg.py::test_qg_spill_trim_at_capacity -m gpu > $O/trim.log 2>&1; tail -5 $O/trim.log
+timeout -k 10 600 python -u -m pytest -x -v --timeout 180 --timeout-method thread tests/test_gpu_qg.py \
+  tests/test_gpu_serve.py tests/test_gpu_lookahead.py -m gpu --deselect tests/test_gpu_qg.py::test_qg_spill_trim_at_capacity \
+  > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 600 python -u bench.py --mode qg --graph anng --qg-expansions 2,3,4,6 --steps 5 --warmup 1 \
+  --cpu-seconds 10 --latency-queries 0 --anng-line off --c3-line off --qg-line off > $O/qg.json 2> $O/qg.log \
+  || { tail -30 $O/qg.log; exit 1; }
+python3 scripts/jline.py $O/qg.json qg

@@ -58,8 +58,10 @@ with open(os.path.join(d, name + "_kernel_stats.csv")) as f:
             avg_ns = float(row["AverageNs"])
 search_ns = None
 tpath = os.path.join(d, name + "_kernel_trace.csv")
-if dps > 1 and os.path.exists(tpath):
-    # per search: the last searches' dispatches in the trace, summed per search
+if os.path.exists(tpath):
+    # per search, over the timed configuration's dispatches only (the last
+    # searches' in the trace, summed per search): the stats file's average
+    # also covers the epsilon sweep's launches of other sizes
     with open(tpath) as f:
         rs = [r for r in csv.DictReader(f) if ksub in r["Kernel_Name"]]
     rs.sort(key=lambda r: int(r["Dispatch_Id"]))

@@ -28,3 +28,30 @@ def test_bound_from_counters():
     assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 560, "SQ_ACTIVE_INST_VALU": 100}) == "latency"
     assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 300, "SQ_ACTIVE_INST_VALU": 600}) == "valu"
     assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 300, "SQ_ACTIVE_INST_VALU": 100}) == "hbm"
+    # most algorithmic bytes from an Infinity-Cache-resident table (the C2 filter copy)
+    assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 495, "SQ_ACTIVE_INST_VALU": 100},
+                                     0.90) == "infinity-cache"
+    assert bench.bound_from_counters({"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 560, "SQ_ACTIVE_INST_VALU": 100},
+                                     0.90) == "latency"
+
+
+def test_run_reaped_terminates_leftovers(tmp_path):
+    """A child's own leftovers (here a background sleep it does not wait for)
+    are terminated with its process group once it exits."""
+    import time
+    pidfile = tmp_path / "pid"
+    rc, out, _ = bench.run_reaped(["bash", "-c", "sleep 60 & echo $! > %s; echo done" % pidfile], 30,
+                                  capture_stderr=True, what="test child")
+    assert rc == 0 and out.strip() == "done"
+    pid = int(pidfile.read_text())
+    for _ in range(50):
+        try:
+            with open("/proc/%d/stat" % pid) as f:
+                state = f.read().rsplit(")", 1)[1].split()[0]
+        except OSError:
+            break
+        if state == "Z":
+            break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("the leftover sleep survived its group")

@@ -13,7 +13,7 @@ import pytest
 
 import ngt_files as F
 import oracle_py as O
-from ngt_amd.device import SEED_GIVEN, SEED_TREE, DeviceIndex
+from ngt_amd.device import SEED_GIVEN, SEED_TREE, DeviceIndex, NativeError
 
 pytestmark = pytest.mark.gpu
 
@@ -154,6 +154,54 @@ def test_qg_overflow_paths_exact(monkeypatch, ht, cq):
             assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32))
             assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt]
     ix.close()
+
+
+def test_qg_spill_trim_at_capacity(monkeypatch):
+    """A full HBM spill first drops its keys beyond the exploration radius
+    (they can never be popped) and flags 'spill capacity exceeded' only if
+    that frees nothing.  The unchecked set's peak (counter 5) at
+    the default capacity sizes the runs: below the peak spill some capacity
+    must give the oracle's exact results only after trims (counter 7 > 0),
+    i.e. where the untrimmed spill would have overflowed; smaller ones may
+    still overflow, and must say so."""
+    monkeypatch.setenv("NGT_AMD_CQ_CAP", "64")
+    qg, rows, valid, offs, ids, tree, prop, z, meta, dim, maxe = state("c1_qg")
+    rng = np.random.default_rng(11)
+    qs = z["queries"].astype(np.float32)
+    seeds = [rng.choice(np.arange(1, rows.shape[0]), 10, replace=False).astype(np.uint32) for _ in qs]
+    outcome = []
+    # large result sets (k x expansion = 300): the radius stays unbounded until
+    # 300 ids are accepted, so the keys spilled meanwhile are mostly beyond the
+    # radius once it forms -- the keys a trim drops
+    for k, eps, exp in [(30, 0.0, 10.0), (100, 0.05, 3.0), (60, 0.1, 5.0)]:
+        ref = [O.qg_search(qg, rows, q, seeds[qi], k, np.float32(eps), np.float32(exp)) for qi, q in enumerate(qs)]
+        monkeypatch.delenv("NGT_AMD_SPILL_CAP", raising=False)
+        ix = device_qg("c1_qg")
+        _, _, _, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_GIVEN, seeds=seeds,
+                                    visited_hash_log2=0)
+        ix.close()
+        peak_spill = int(cnt[:, 5].max()) - 64 - 64  # head and tail capacities
+        for f in (0.9, 0.75, 0.6, 0.45, 0.3):
+            cap = max(40, int(peak_spill * f))
+            monkeypatch.setenv("NGT_AMD_SPILL_CAP", str(cap))
+            ix = device_qg("c1_qg")
+            try:
+                gi, gd, gn, cnt = ix.qg_search(qs, k=k, epsilon=eps, result_expansion=exp, seed_mode=SEED_GIVEN,
+                                               seeds=seeds, visited_hash_log2=0)
+            except NativeError as e:
+                assert "spill capacity" in str(e), e
+                outcome.append((k, eps, exp, peak_spill, cap, "overflow"))
+                ix.close()
+                continue
+            ix.close()
+            for qi in range(len(qs)):
+                oid, od, ocnt = ref[qi]
+                assert list(gi[qi, :gn[qi]]) == list(oid), (k, cap, qi)
+                assert np.array_equal(gd[qi, :gn[qi]].view(np.uint32), od.view(np.uint32)), (k, cap, qi)
+                assert [int(x) for x in cnt[qi, :4]] == [int(x) for x in ocnt], (k, cap, qi)
+            outcome.append((k, eps, exp, peak_spill, cap, "exact", int(cnt[:, 7].sum())))
+    print(outcome)
+    assert any(o[5] == "exact" and o[6] > 0 for o in outcome), outcome
 
 
 def test_qg_edge_cases():
