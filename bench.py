@@ -368,7 +368,12 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-launches", type=int, default=0,
                     help="after the epsilon is set: run this many launches of the timed configuration and exit")
-    ap.add_argument("--streams", type=int, default=3, help="HIP streams consecutive steps alternate over")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams consecutive steps alternate over (default 3, or 1 when three streams' "
+                         "visited scratch -- rows x 16 waves per CU each -- would exceed a quarter of the HBM)")
+    ap.add_argument("--streams-ab", type=str, default="",
+                    help="experiment: after the timed steps, time the same steps over each of these stream counts "
+                         "(logged and reported as config.stream_ab_ms_per_step; the line's value is --streams)")
     ap.add_argument("--anng-line", choices=["auto", "on", "off"], default="auto",
                     help="attach the NGT-built index's line (a child run of --graph anng) as the 'anng' key; "
                          "auto = on for the default single-GPU C2 run")
@@ -430,6 +435,13 @@ def main():
         if n_ranks != args.gpus:
             raise SystemExit("bench: %d ranks joined RCCL, --gpus %d" % (n_ranks, args.gpus))
 
+    if args.streams is None:
+        # every stream has its own launch context with slots x rows visited
+        # bytes; three of them at 12.5M rows (51 GB each) squeeze each other's
+        # slot counts, and a long launch gains nothing from the overlap
+        props = torch.cuda.get_device_properties(dev)
+        per_ctx = (args.n + 1) * 16 * props.multi_processor_count
+        args.streams = 3 if 3 * per_ctx <= 0.25 * props.total_memory else 1
     from ngt_amd.device import COUNTERS, SEED_GIVEN, SEED_TREE, DeviceIndex
     if args.mode == "capi":
         return capi_bench(args, torch, dev, result_out)
@@ -548,7 +560,8 @@ def main():
     # consecutive steps alternate over `--streams` HIP streams (each with its
     # own output buffers and, inside the library, its own launch scratch), so
     # a step's kernel starts while the previous step's last queries drain
-    nstreams = 1 if shard else max(1, args.streams)
+    stream_ab = [int(x) for x in args.streams_ab.split(",")] if args.streams_ab else []
+    nstreams = 1 if shard else max([1, args.streams] + stream_ab)
     streams = [stream] + [torch.cuda.Stream(dev).cuda_stream for _ in range(nstreams - 1)]
     bufs = [(torch.zeros((NQ, K), dtype=torch.int32, device=dev), torch.zeros((NQ, K), dtype=torch.float32, device=dev),
              torch.zeros((NQ,), dtype=torch.int32, device=dev), torch.zeros((NQ, COUNTERS), dtype=torch.int64, device=dev))
@@ -693,20 +706,33 @@ def main():
                           "launches_before": len(sweep), "kernel_ms_last": ix.last_search_kernel_ms()}),
               file=result_out, flush=True)
         return
-    for i in range(max(args.warmup, nstreams)):
-        run(chosen, i % nstreams)
+    ns_timed = 1 if shard else max(1, args.streams)
+    for i in range(max(args.warmup, ns_timed)):
+        run(chosen, i % ns_timed)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        run(chosen, i % nstreams)
+        run(chosen, i % ns_timed)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    stream_ms = {}
+    for n in stream_ab:
+        # EXPERIMENT (not the line's value): the same steps alternating over n streams
+        for i in range(max(args.warmup, n)):
+            run(chosen, i % n)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            run(chosen, i % n)
+        torch.cuda.synchronize()
+        stream_ms[n] = (time.perf_counter() - t1) / args.steps * 1e3
+        log("streams %d: %.2f ms per step" % (n, stream_ms[n]))
     # per-launch duration of the search kernel: HIP events recorded by the
     # library around the kernel on the stream it runs on
     kms = []
@@ -939,7 +965,7 @@ def main():
                        "parallelism": ("shards x%d" % world) if shard else ("replicas x%d" % world),
                        "distance_filter": ("1-byte filter copy (lower bound rejects neighbours outside the "
                                            "exploration radius; exact f32 rows for the rest)" if filtered else "none"),
-                       "streams": nstreams},
+                       "streams": ns_timed},
             "roofline": {"bound": "unmeasured", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": alg_bytes,
@@ -974,6 +1000,8 @@ def main():
             "parity_sample": parity,
             "sweep": sweep,
         }
+        if stream_ms:
+            line["config"]["stream_ab_ms_per_step"] = stream_ms
         if scan is not None:
             line["exact_scan"] = scan
         if build_s is not None:

@@ -397,6 +397,12 @@ int ngt_amd::ensure_vis_scratch(ngt_amd_index* ix, SearchCtx* c, size_t lds, uin
   const uint64_t per_slot = stride + (uint64_t)ix->spill_cap * 8 + 4;
   const uint64_t max_slots = (uint64_t)(avail * mem_frac) / per_slot;
   if (max_slots < 1) return fail("search: no HBM left for the visited scratch (%llu rows)", (unsigned long long)ix->nrows);
+  // a context that already holds as many slots as the memory allows now keeps
+  // them: reallocating to fewer (other contexts took memory meanwhile) would
+  // only cost a synchronizing free + alloc per launch and fewer waves
+  // (the 12.5M-row NGTQG line on three streams: 0.7-1.2 s gaps between
+  // launches, grids of 1,000-3,300 slots; profiles/r6e)
+  if (stride == c->vis_stride && c->spill.p && max_slots <= c->slots) return 0;
   const uint32_t slots = (uint32_t)std::min<uint64_t>(std::max(want, c->slots), max_slots);
   if (slots == c->slots && stride == c->vis_stride && c->spill.p) return 0;
   c->vis.release();
