@@ -307,6 +307,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--shard-n", type=int, default=1_250_000, help="shard line: objects per shard")
     ap.add_argument("--shard-count", type=int, default=8, help="shard line: shards of the whole index")
+    ap.add_argument("--shard-qg-line", choices=["on", "off"], default="on",
+                    help="with the shard line: also C5's form (every shard an NGTQG quantized graph) over the same "
+                         "shards, as its 'qg_form' key")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: gloo ranks time rank-dependent sleeps (no search)")
     ap.add_argument("--shard-line", choices=["auto", "on", "off"], default="auto",
@@ -1104,9 +1107,12 @@ def main():
         sargs.shards_per_gpu = max(1, args.shard_count // world)
         sargs.steps = max(3, min(args.steps, 10))
         sargs.warmup = 1
-        log("shard line: C4 as %d x %d shards of %d objects" % (world, sargs.shards_per_gpu, sargs.n))
+        log("shard line: C4 as %d x %d shards of %d objects%s" % (
+            world, sargs.shards_per_gpu, sargs.n, ", then C5's NGTQG form over the same shards"
+            if args.shard_qg_line == "on" else ""))
         t0 = time.time()
-        sl = shard_bench(sargs, torch, dist, dev, rank, world, local, None, False, emit=False)
+        sl = shard_bench(sargs, torch, dist, dev, rank, world, local, None, False, emit=False,
+                         also_qg=args.shard_qg_line == "on")
         if rank == 0:
             sl.pop("sweep", None)
             sl["scaling"] = "strong"
@@ -1626,7 +1632,7 @@ def capi_bench(args, torch, dev, result_out):
     ix.close()
 
 
-def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm, emit=True):
+def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm, emit=True, also_qg=False):
     """C4's and C5's form: the object repository as
     world x S shards of --n objects, rank r holding shards r*S .. r*S+S-1
     (global ids offset by shard * n), every shard an independent index with
@@ -1694,176 +1700,208 @@ def shard_bench(args, torch, dist, dev, rank, world, local, result_out, qgm, emi
     d_seeds = torch.from_numpy(seeds.reshape(-1).astype(np.int32)).to(dev)
     d_soff = torch.arange(0, NQ + 1, dtype=torch.int64, device=dev) * args.seed_size
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
-    out_i, out_d, out_n = buffers()
-    cnt = torch.zeros((S, NQ, COUNTERS), dtype=torch.int64, device=dev)
-    merged = {}
+    def measure_form(qgm):
+        """Tune, time and check one form of the sharded index (exact graph
+        search, or NGTQG over the same shards); rank 0 gets its line."""
+        out_i, out_d, out_n = buffers()
+        cnt = torch.zeros((S, NQ, COUNTERS), dtype=torch.int64, device=dev)
+        merged = {}
 
-    def search_shard(s, eps, st, visited):
-        ix = shards[s]["ix"]
-        if qgm:
-            ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, out_i[s].data_ptr(), out_d[s].data_ptr(),
-                                out_n[s].data_ptr(), cnt[s].data_ptr(), k=K, epsilon=eps,
-                                result_expansion=args.expansion, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
-                                d_seed_off=d_soff.data_ptr(), stream=st, visited_hash_log2=visited)
-        else:
-            ix.search_device(qdev.data_ptr(), dp * 4, NQ, out_i[s].data_ptr(), out_d[s].data_ptr(),
-                             out_n[s].data_ptr(), cnt[s].data_ptr(), k=K, epsilon=eps, edge_size=0,
-                             seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
-                             stream=st, visited_hash_log2=visited)
+        def search_shard(s, eps, st, visited):
+            ix = shards[s]["ix"]
+            if qgm:
+                ix.qg_search_device(qdev.data_ptr(), dp * 4, NQ, out_i[s].data_ptr(), out_d[s].data_ptr(),
+                                    out_n[s].data_ptr(), cnt[s].data_ptr(), k=K, epsilon=eps,
+                                    result_expansion=args.expansion, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                                    d_seed_off=d_soff.data_ptr(), stream=st, visited_hash_log2=visited)
+            else:
+                ix.search_device(qdev.data_ptr(), dp * 4, NQ, out_i[s].data_ptr(), out_d[s].data_ptr(),
+                                 out_n[s].data_ptr(), cnt[s].data_ptr(), k=K, epsilon=eps, edge_size=0,
+                                 seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(), d_seed_off=d_soff.data_ptr(),
+                                 stream=st, visited_hash_log2=visited)
 
-    def run(eps, visited=None):
-        visited = args.visited if visited is None else visited
-        # the shard streams wait for the previous step's pack (it reads out_*)
-        for st in streams:
-            st.wait_stream(main)
-        for s in range(S):
-            search_shard(s, eps, streams[s].cuda_stream, visited)
-        for st in streams:
-            main.wait_stream(st)
-        merged["r"] = sx.merge_local(out_i, out_d, out_n, K, main.cuda_stream)
+        # the NGTQG search marks accepted ids by definition (QuantizedGraph.h:241-266)
+        vis_default = -1 if qgm and args.visited == -2 else args.visited
 
-    sweep = []
+        def run(eps, visited=None):
+            visited = vis_default if visited is None else visited
+            # the shard streams wait for the previous step's pack (it reads out_*)
+            for st in streams:
+                st.wait_stream(main)
+            for s in range(S):
+                search_shard(s, eps, streams[s].cuda_stream, visited)
+            for st in streams:
+                main.wait_stream(st)
+            merged["r"] = sx.merge_local(out_i, out_d, out_n, K, main.cuda_stream)
 
-    def measure(eps):
-        run(eps)
-        torch.cuda.synchronize()
-        r = recall_at(merged["r"][0].cpu().numpy(), gt, K)
-        sweep.append((round(eps, 5), r, None, NQ))
-        log("eps %.4f merged recall@%d %.4f" % (eps, K, r))
-        return r
+        sweep = []
 
-    chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None)
-    rec = measure(chosen)
-    for _ in range(20):
-        if rec >= args.target or args.eps:
-            break
-        chosen = round(chosen * 1.02 + 1e-4, 5)
-        rec = measure(chosen)
-    if args.pmc_launches:
-        # counter passes: exactly this many more steps of the timed
-        # configuration (S shard searches each), nothing else of the bench
-        for _ in range(args.pmc_launches):
-            run(chosen)
+        def measure(eps):
+            run(eps)
             torch.cuda.synchronize()
-        if rank == 0:
-            print(json.dumps({"pmc_launches": args.pmc_launches, "shards_per_gpu": S, "epsilon": chosen,
-                              "recall_at_10": rec}), file=result_out, flush=True)
+            r = recall_at(merged["r"][0].cpu().numpy(), gt, K)
+            sweep.append((round(eps, 5), r, None, NQ))
+            log("eps %.4f merged recall@%d %.4f" % (eps, K, r))
+            return r
+
+        chosen = tune_epsilon(measure, args.target, [float(x) for x in args.eps.split(",")] if args.eps else None)
+        rec = measure(chosen)
+        for _ in range(20):
+            if rec >= args.target or args.eps:
+                break
+            chosen = round(chosen * 1.02 + 1e-4, 5)
+            rec = measure(chosen)
+        if args.pmc_launches:
+            # counter passes: exactly this many more steps of the timed
+            # configuration (S shard searches each), nothing else of the bench
+            for _ in range(args.pmc_launches):
+                run(chosen)
+                torch.cuda.synchronize()
+            if rank == 0:
+                print(json.dumps({"pmc_launches": args.pmc_launches, "shards_per_gpu": S, "epsilon": chosen,
+                                  "recall_at_10": rec}), file=result_out, flush=True)
+            if dist is not None:
+                dist.destroy_process_group()
+            return
+        for _ in range(max(1, args.warmup)):
+            run(chosen)
+        torch.cuda.synchronize()
         if dist is not None:
-            dist.destroy_process_group()
-        return
-    for _ in range(max(1, args.warmup)):
-        run(chosen)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        run(chosen)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t1
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    qps = NQ * args.steps / elapsed
-    res = [x.clone() for x in merged["r"]]
-    # per-launch kernel time: each shard's search alone on the main stream
-    kms = []
-    for s in range(S):
-        search_shard(s, chosen, main.cuda_stream, args.visited)
+            dist.barrier()
         torch.cuda.synchronize()
-        kms.append(shards[s]["ix"].last_search_kernel_ms())
-    filtered = (not qgm) and ix0.last_search_filtered()
-    # the schedule budget of those launches (0: single dispatches)
-    budget = 0 if qgm else shards[S - 1]["ix"].last_search_budget()
-    split = None  # (the exact mode's filter-copy split is not kept per shard)
-    if not qgm and args.visited == -2:
-        # the reference's distinct distance counts (every evaluated id in the
-        # visited set) for the algorithmic bytes; the results must not change
-        run(chosen, visited=-1)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            run(chosen)
         torch.cuda.synchronize()
-        same = all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip(res, merged["r"]))
-        if not same:
-            raise SystemExit("bench: accepted-only visited set changed the merged results")
-    c = cnt.cpu().numpy().astype(np.float64).reshape(S * NQ, COUNTERS)
-    if qgm:
-        me = (D + 1) // 2 * 2
-        alg_bytes = (c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4
-                     + S * NQ * (dp * 4 + K * 8))
-        kname = "ngt_qg_search_kernel"
-    elif filtered:
-        alg_bytes = ((c[:, 0] - c[:, 7]).sum() * dp + (c[:, 7] + c[:, 6]).sum() * dp * 4 + c[:, 4].sum() * 4
-                     + S * NQ * (dp * 4 + K * 8))
-        kname = "ngt_graph_search_kernel"
-    else:
-        alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + S * NQ * (dp * 4 + K * 8)
-        kname = "ngt_graph_search_kernel"
-    kernel_ms = float(np.mean(kms))
-    per_launch = alg_bytes / S
-    achieved = per_launch / (kernel_ms * 1e-3) / 1e9
-    literal = literal_bytes(c, dp, S * NQ, K, qgm, D) / S
-
-    cpu = parity = None
-    if not args.no_cpu:
-        # every rank checks its own shards against the oracle; with several
-        # ranks the candidates are all-gathered and every rank checks the merge
-        cpu, parity = shard_parity_sample(args, shards, qdev, seeds, chosen, res, qgm, dist=dist)
-
-    if rank == 0:
-        total = N * S * world
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t1
+        if dist is not None:
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        qps = NQ * args.steps / elapsed
+        res = [x.clone() for x in merged["r"]]
+        # per-launch kernel time: each shard's search alone on the main stream
+        kms = []
+        for s in range(S):
+            search_shard(s, chosen, main.cuda_stream, vis_default)
+            torch.cuda.synchronize()
+            kms.append(shards[s]["ix"].last_search_kernel_ms())
+        filtered = (not qgm) and ix0.last_search_filtered()
+        # the schedule budget of those launches (0: single dispatches)
+        budget = 0 if qgm else shards[S - 1]["ix"].last_search_budget()
+        split = None  # (the exact mode's filter-copy split is not kept per shard)
+        if not qgm and args.visited == -2:
+            # the reference's distinct distance counts (every evaluated id in the
+            # visited set) for the algorithmic bytes; the results must not change
+            run(chosen, visited=-1)
+            torch.cuda.synchronize()
+            same = all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip(res, merged["r"]))
+            if not same:
+                raise SystemExit("bench: accepted-only visited set changed the merged results")
+        c = cnt.cpu().numpy().astype(np.float64).reshape(S * NQ, COUNTERS)
         if qgm:
-            metric_name = "QPS at recall@10=0.95, %d x %d-d NGTQG sharded over %d GPUs" % (total, D, world)
-            workload = ("C5 form: %d objects per GPU as %d NGTQG shards of %d (dsub=1, M=%d, result_expansion %g), "
-                        "%d GPUs, %d queries/step over all shards, k=%d, one packed RCCL all-gather of per-shard "
-                        "top-k + device merge" % (N * S, S, N, D, args.expansion, world, NQ, K))
+            me = (D + 1) // 2 * 2
+            alg_bytes = (c[:, 4].sum() * 8 * me + c[:, 0].sum() * 4 + c[:, 3].sum() * dp * 4
+                         + S * NQ * (dp * 4 + K * 8))
+            kname = "ngt_qg_search_kernel"
+        elif filtered:
+            alg_bytes = ((c[:, 0] - c[:, 7]).sum() * dp + (c[:, 7] + c[:, 6]).sum() * dp * 4 + c[:, 4].sum() * 4
+                         + S * NQ * (dp * 4 + K * 8))
+            kname = "ngt_graph_search_kernel"
         else:
-            metric_name = "QPS at recall@10=0.95, %d x %d-d float L2 sharded over %d GPUs" % (total, D, world)
-            workload = ("C4 form: %d objects per GPU as %d shards of %d, %d GPUs, %d queries/step over all shards, "
-                        "k=%d, one packed RCCL all-gather of per-shard top-k + device merge" % (
-                            N * S, S, N, world, NQ, K))
-        line = {
-            "metric": metric_name, "value": qps, "unit": "queries/s", "n_gpus": dist.get_world_size() if dist is not None else 1,
-            "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32" if not qgm else "u4-adc/u8-lut/f32-rerank",
-            "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
-            "config": {"workload": workload, "objects_total": total, "shards_per_gpu": S, "objects_per_shard": N,
-                       "recall_at_10": rec, "epsilon": chosen,
-                       "graph": "kNN%d out%d in%d max%d per shard" % (args.knn, args.out_deg, args.in_deg,
-                                                                     args.max_deg),
-                       "seeds": "getRandomSeeds (%d)" % args.seed_size, "setup_s": setup_s,
-                       "distance_filter": "1-byte filter copy" if filtered else "none",
-                       "parallelism": "shards x%d (%d per GPU, one stream each)" % (S * world, S),
-                       "distance_computations_per_query_per_shard": float(c[:, 0].mean()),
-                       "expansions_per_query_per_shard": float(c[:, 2].mean())},
-            "roofline": {"bound": "unmeasured", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,
-                         "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": per_launch,
-                         "bytes_definition": ("the filtered kernel's own bytes (DESIGN.md 4)" if filtered
-                                              else "SURVEY.md 8(d) B(q)"),
-                         "literal_bytes_per_launch": literal,
-                         "effective_gbs_literal": literal / (kernel_ms * 1e-3) / 1e9,
-                         "effective_frac_literal": literal / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                         "infinity_cache_resident_share": (
-                             (c[:, 0] - c[:, 7]).sum() * dp / S / per_launch
-                             if filtered and (N + 1) * dp <= 256 * 2 ** 20 else 0.0),
-                         "what": "one shard's search launch alone (mean over the %d local shards)" % S,
-                         "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
-                         "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
-                         "bytes_split": split,
-                         # the probe-and-resume schedule: one search = a probe dispatch (every query
-                         # paused after `budget` expansions) + a resume dispatch, longest predicted first;
-                         # kernel_ms spans both (ngt_amd_api.cpp run_search)
-                         "search_dispatches": 2 if budget else 1,
-                         "schedule_budget": budget},
-            "cpu_baseline": cpu, "parity_sample": parity, "sweep": sweep}
-        if qgm:
-            line["config"]["result_expansion"] = args.expansion
+            alg_bytes = c[:, 0].sum() * dp * 4 + c[:, 4].sum() * 4 + S * NQ * (dp * 4 + K * 8)
+            kname = "ngt_graph_search_kernel"
+        kernel_ms = float(np.mean(kms))
+        per_launch = alg_bytes / S
+        achieved = per_launch / (kernel_ms * 1e-3) / 1e9
+        literal = literal_bytes(c, dp, S * NQ, K, qgm, D) / S
+
+        cpu = parity = None
+        if not args.no_cpu:
+            # every rank checks its own shards against the oracle; with several
+            # ranks the candidates are all-gathered and every rank checks the merge
+            cpu, parity = shard_parity_sample(args, shards, qdev, seeds, chosen, res, qgm, dist=dist)
+
+        if rank == 0:
+            total = N * S * world
+            if qgm:
+                metric_name = "QPS at recall@10=0.95, %d x %d-d NGTQG sharded over %d GPUs" % (total, D, world)
+                workload = ("C5 form: %d objects per GPU as %d NGTQG shards of %d (dsub=1, M=%d, result_expansion %g), "
+                            "%d GPUs, %d queries/step over all shards, k=%d, one packed RCCL all-gather of per-shard "
+                            "top-k + device merge" % (N * S, S, N, D, args.expansion, world, NQ, K))
+            else:
+                metric_name = "QPS at recall@10=0.95, %d x %d-d float L2 sharded over %d GPUs" % (total, D, world)
+                workload = ("C4 form: %d objects per GPU as %d shards of %d, %d GPUs, %d queries/step over all shards, "
+                            "k=%d, one packed RCCL all-gather of per-shard top-k + device merge" % (
+                                N * S, S, N, world, NQ, K))
+            line = {
+                "metric": metric_name, "value": qps, "unit": "queries/s", "n_gpus": dist.get_world_size() if dist is not None else 1,
+                "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32" if not qgm else "u4-adc/u8-lut/f32-rerank",
+                "data": "synthetic (splitmix64 U[0,1), seed 0x4E4754)",
+                "config": {"workload": workload, "objects_total": total, "shards_per_gpu": S, "objects_per_shard": N,
+                           "recall_at_10": rec, "epsilon": chosen,
+                           "graph": "kNN%d out%d in%d max%d per shard" % (args.knn, args.out_deg, args.in_deg,
+                                                                         args.max_deg),
+                           "seeds": "getRandomSeeds (%d)" % args.seed_size, "setup_s": setup_s,
+                           "distance_filter": "1-byte filter copy" if filtered else "none",
+                           "parallelism": "shards x%d (%d per GPU, one stream each)" % (S * world, S),
+                           "distance_computations_per_query_per_shard": float(c[:, 0].mean()),
+                           "expansions_per_query_per_shard": float(c[:, 2].mean())},
+                "roofline": {"bound": "unmeasured", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,
+                             "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": per_launch,
+                             "bytes_definition": ("the filtered kernel's own bytes (DESIGN.md 4)" if filtered
+                                                  else "SURVEY.md 8(d) B(q)"),
+                             "literal_bytes_per_launch": literal,
+                             "effective_gbs_literal": literal / (kernel_ms * 1e-3) / 1e9,
+                             "effective_frac_literal": literal / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                             "infinity_cache_resident_share": (
+                                 (c[:, 0] - c[:, 7]).sum() * dp / S / per_launch
+                                 if filtered and (N + 1) * dp <= 256 * 2 ** 20 else 0.0),
+                             "what": "one shard's search launch alone (mean over the %d local shards)" % S,
+                             "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,
+                             "frac_per_step": alg_bytes / (elapsed / args.steps) / 1e9 / PEAK_HBM_GBS,
+                             "bytes_split": split,
+                             # the probe-and-resume schedule: one search = a probe dispatch (every query
+                             # paused after `budget` expansions) + a resume dispatch, longest predicted first;
+                             # kernel_ms spans both (ngt_amd_api.cpp run_search)
+                             "search_dispatches": 2 if budget else 1,
+                             "schedule_budget": budget},
+                "cpu_baseline": cpu, "parity_sample": parity, "sweep": sweep}
+            if qgm:
+                line["config"]["result_expansion"] = args.expansion
+        return line if rank == 0 else None
+
+    line = measure_form(qgm)
+    if args.pmc_launches:
+        return
+    if True:
+        if also_qg and not qgm:
+            # C5's form over the same shards: ngtqg quantize of every shard
+            # (kmeansWithNGT codebooks from its first 1,600 objects, encoder,
+            # quantized graph; QuantizedGraph.h:456-475), then the same
+            # tuning, timing, all-gather + merge and oracle parity sample
+            t1 = time.time()
+            for sh in shards:
+                h_base = np.zeros((min(N, 1600) + 1, D), np.float32)
+                h_base[1:] = splitmix_uniform(min(N, 1600), D, BASE_SEED, row0=sh["off"])
+                sh["qg_local"] = sh["ix"].qg_train_ngt(h_base, dsub=1)
+                sh["ix"].qg_encode(return_codes=False)
+                sh["ix"].qg_build_graph(None, args.qg_edges)
+            torch.cuda.synchronize()
+            log("shards quantized (NGTQG) in %.1f s" % (time.time() - t1))
+            qline = measure_form(True)
+            if rank == 0:
+                qline.pop("sweep", None)
+                qline["config"]["quantize_s"] = time.time() - t1
+                line["qg_form"] = qline
+    if rank == 0:
         if not emit:
             return line
         print(json.dumps(line), file=result_out, flush=True)
