@@ -373,7 +373,7 @@ def main():
                     help="after the epsilon is set: run this many launches of the timed configuration and exit")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams consecutive steps alternate over (default 3, or 1 when three streams' "
-                         "visited scratch -- rows x 16 waves per CU each -- would exceed a quarter of the HBM)")
+                         "visited scratch -- rows x 16 waves per CU each -- would exceed 0.6 of the HBM)")
     ap.add_argument("--streams-ab", type=str, default="",
                     help="experiment: after the timed steps, time the same steps over each of these stream counts "
                          "(logged and reported as config.stream_ab_ms_per_step; the line's value is --streams)")
@@ -444,7 +444,7 @@ def main():
         # slot counts, and a long launch gains nothing from the overlap
         props = torch.cuda.get_device_properties(dev)
         per_ctx = (args.n + 1) * 16 * props.multi_processor_count
-        args.streams = 3 if 3 * per_ctx <= 0.25 * props.total_memory else 1
+        args.streams = 3 if 3 * per_ctx <= 0.6 * props.total_memory else 1
     from ngt_amd.device import COUNTERS, SEED_GIVEN, SEED_TREE, DeviceIndex
     if args.mode == "capi":
         return capi_bench(args, torch, dev, result_out)
