@@ -48,6 +48,10 @@ sys.path.insert(0, ROOT)
 
 BASE_SEED = 0x4E4754
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# MI355X_MICROARCH.md 'Indexed rows: gather into LDS': uniformly random rows of a
+# 38 MB table (Infinity-Cache resident) gathered at 8.6 TB/s chip-wide -- the
+# measured rate for a table the Infinity Cache holds (a lower bound of its peak)
+IC_GATHER_GBS = 8600.0
 HEADLINE = "QPS at recall@10=0.95, 1M x 128-d float L2; achieved HBM GB/s vs peak"
 
 
@@ -989,6 +993,14 @@ def main():
                          "hbm_side_gbs": alg_bytes * (1.0 - ic_share(split, alg_bytes)) / (kernel_ms * 1e-3) / 1e9,
                          "hbm_side_frac": (alg_bytes * (1.0 - ic_share(split, alg_bytes)) / (kernel_ms * 1e-3) / 1e9
                                            / PEAK_HBM_GBS),
+                         # the bytes from the Infinity-Cache-resident table against the measured
+                         # random-row gather rate of such a table
+                         "ic_side_gbs": alg_bytes * ic_share(split, alg_bytes) / (kernel_ms * 1e-3) / 1e9,
+                         "ic_side_frac": (alg_bytes * ic_share(split, alg_bytes) / (kernel_ms * 1e-3) / 1e9
+                                          / IC_GATHER_GBS),
+                         "ic_side_frac_per_step": (alg_bytes * ic_share(split, alg_bytes) / (elapsed / args.steps)
+                                                   / 1e9 / IC_GATHER_GBS),
+                         "ic_gather_peak_gbs": IC_GATHER_GBS,
                          # the same bytes over the whole step with launches overlapping on the streams
                          # (a single launch's last round of queries leaves the GPU part-empty)
                          "achieved_per_step": alg_bytes / (elapsed / args.steps) / 1e9,

@@ -170,6 +170,20 @@ static int qg_pack(ngt_amd_index* ix) {
   return 0;
 }
 
+// The packed records are an optional speedup over the fixed slabs the graph
+// build leaves in place: a pack that fails (allocation, upload, kernel) leaves
+// the index unpacked, and searches read the slabs.
+static int qg_pack_or_slabs(ngt_amd_index* ix) {
+  if (qg_pack(ix) == 0) return 0;
+  QgState& q = ix->qg;
+  q.packed = false;
+  q.recs.release();
+  q.qkw.release();
+  q.rec_bytes = 0;
+  (void)hipGetLastError();  // the failed call's sticky error
+  return 0;
+}
+
 extern "C" uint64_t ngt_amd_qg_record_bytes(const ngt_amd_index* ix) {
   return ix && ix->qg.has_graph && ix->qg.packed ? ix->qg.rec_bytes : 0;
 }
@@ -211,7 +225,7 @@ extern "C" int ngt_amd_qg_build_graph(ngt_amd_index* ix, const uint8_t* local_co
   HIP_OK(launch_qg_build(a, ix->stream));
   HIP_OK(hipStreamSynchronize(ix->stream));
   q.has_graph = true;
-  return qg_pack(ix);
+  return qg_pack_or_slabs(ix);
 }
 
 extern "C" int ngt_amd_qg_set_graph(ngt_amd_index* ix, const uint64_t* qoff, const uint32_t* qids,
@@ -243,7 +257,7 @@ extern "C" int ngt_amd_qg_set_graph(ngt_amd_index* ix, const uint64_t* qoff, con
   HIP_OK(hipMemcpy(q.qids.p, hid.data(), hid.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(q.qcodes.p, hcode.data(), hcode.size(), hipMemcpyHostToDevice));
   q.has_graph = true;
-  return qg_pack(ix);
+  return qg_pack_or_slabs(ix);
 }
 
 extern "C" uint32_t ngt_amd_qg_max_degree(const ngt_amd_index* ix) {
