@@ -1053,13 +1053,19 @@ def main():
                     "SQ_INSTS_LDS": cn.get("SQ_INSTS_LDS"),
                     "trace_avg_kernel_ms": tentry.get("trace_avg_kernel_ms")})
                 # what bounds the kernel, from the wave-cycle partition
-                line["roofline"]["bound"] = bound_from_counters(cn, ic_share(split, alg_bytes))
+                si = tentry.get("simd_issue")
+                if si:
+                    # the SIMDs' issue in measured (GRBM) cycles, scripts/pmc_clk.sh
+                    line["roofline"]["counters"]["simd_issue"] = si
+                line["roofline"]["bound"] = bound_from_counters(cn, ic_share(split, alg_bytes), si)
                 line["roofline"]["bound_note"] = (
-                    "from the SQ wave-cycle partition and the byte split: 'latency' when >= 0.5 of the "
-                    "wave-cycles are parked on s_waitcnt (dependent gathers), 'valu' when VALU issues on "
-                    ">= 0.5, 'infinity-cache' when most algorithmic bytes come from a table the 256 MiB "
-                    "Infinity Cache holds, else 'hbm'; achieved/frac are against the 8 TB/s HBM figure, "
-                    "hbm_side_frac counts only the bytes from tables beyond the Infinity Cache")
+                    "from the SQ counters and the byte split: 'issue' when the SIMDs issue in >= 0.7 of their "
+                    "GRBM-measured cycles (counters.simd_issue), 'latency' when >= 0.5 of the wave-cycles are "
+                    "parked on s_waitcnt (dependent gathers), 'valu' when VALU issues on >= 0.5, "
+                    "'infinity-cache' when most algorithmic bytes come from a table the 256 MiB Infinity Cache "
+                    "holds, else 'hbm'; achieved/frac are against the 8 TB/s HBM figure, hbm_side_frac counts "
+                    "only the bytes from tables beyond the Infinity Cache, ic_side_frac the IC-resident bytes "
+                    "against the measured 8.6 TB/s Infinity-Cache gather rate")
         if qgm:
             line["config"]["result_expansion"] = args.expansion
             if expansion_sweep is not None:
@@ -1154,14 +1160,18 @@ def ic_share(split, alg_bytes):
     return float(split["filter_copy_bytes"] / alg_bytes)
 
 
-def bound_from_counters(cn, ic_resident_share=0.0):
-    """What bounds the kernel, from the SQ wave-cycle partition
-    (MI355X_MICROARCH.md rocprofv3 PMC): more than half the wave-cycles parked
-    on s_waitcnt = dependent-gather latency; else VALU-issue bound if VALU
-    issues on more than half; else the memory system -- the Infinity Cache
-    when most of the algorithmic bytes come from a table it holds (the C2
-    filter copy), HBM otherwise."""
+def bound_from_counters(cn, ic_resident_share=0.0, simd_issue=None):
+    """What bounds the kernel, from the SQ counters (MI355X_MICROARCH.md
+    rocprofv3 PMC): the SIMDs issuing in at least 0.7 of their cycles (the
+    GRBM-clocked pass, scripts/pmc_clk.sh) = instruction issue, however long
+    each wave waits -- the other waves of its SIMD fill the gaps; else more
+    than half the wave-cycles parked on s_waitcnt = dependent-gather latency;
+    else VALU-issue bound if VALU issues on more than half; else the memory
+    system -- the Infinity Cache when most of the algorithmic bytes come from
+    a table it holds (the C2 filter copy), HBM otherwise."""
     w = cn["SQ_WAVE_CYCLES"]
+    if simd_issue and simd_issue.get("simd_issue_util", 0.0) >= 0.7:
+        return "issue"
     if cn.get("SQ_WAIT_ANY", 0) / w >= 0.5:
         return "latency"
     if cn.get("SQ_ACTIVE_INST_VALU", 0) / w >= 0.5:

@@ -55,3 +55,13 @@ def test_run_reaped_terminates_leftovers(tmp_path):
         time.sleep(0.1)
     else:
         raise AssertionError("the leftover sleep survived its group")
+
+
+def test_bound_issue_from_clocked_pass():
+    """A SIMD issuing in >= 0.7 of its measured cycles is issue-bound even when
+    its waves wait on memory most of the time (the other waves fill in)."""
+    w = 1000.0
+    cn = {"SQ_WAVE_CYCLES": w, "SQ_WAIT_ANY": 650, "SQ_ACTIVE_INST_VALU": 150}
+    assert bench.bound_from_counters(cn, 0.0, {"simd_issue_util": 0.78}) == "issue"
+    assert bench.bound_from_counters(cn, 0.0, {"simd_issue_util": 0.58}) == "latency"
+    assert bench.bound_from_counters(cn, 0.0, None) == "latency"
