@@ -65,3 +65,18 @@ def test_bound_issue_from_clocked_pass():
     assert bench.bound_from_counters(cn, 0.0, {"simd_issue_util": 0.78}) == "issue"
     assert bench.bound_from_counters(cn, 0.0, {"simd_issue_util": 0.58}) == "latency"
     assert bench.bound_from_counters(cn, 0.0, None) == "latency"
+
+
+def test_pick_expansion():
+    sw = [{"result_expansion": 2.0, "epsilon": 0.106, "recall_at_10": 0.955, "kernel_ms": 85.0},
+          {"result_expansion": 3.0, "epsilon": 0.098, "recall_at_10": 0.955, "kernel_ms": 77.5},
+          {"result_expansion": 4.0, "epsilon": 0.093, "recall_at_10": 0.957, "kernel_ms": 79.2},
+          {"result_expansion": 6.0, "epsilon": 0.085, "recall_at_10": 0.955, "kernel_ms": 76.5}]
+    # 3.0 is within 3 % of the fastest (6.0): the tie goes to the default
+    assert bench.pick_expansion(sw, 0.95)["result_expansion"] == 3.0
+    # a clear winner is taken
+    sw[3]["kernel_ms"] = 60.0
+    assert bench.pick_expansion(sw, 0.95)["result_expansion"] == 6.0
+    # one below the target is skipped while another reaches it
+    sw[3]["recall_at_10"] = 0.94
+    assert bench.pick_expansion(sw, 0.95)["result_expansion"] == 3.0

@@ -106,6 +106,24 @@ def test_visited_scratch_full_occupancy_at_shard_size():
     # a graph without edges returns exactly the seed
     assert np.all(on.cpu().numpy() == 1)
     assert np.array_equal(oi[:, 0].cpu().numpy(), seeds)
+    # three more streams, each a launch context of its own competing for the
+    # same HBM: a context keeps the slots it got (round 6: it used to
+    # reallocate to a smaller count on every launch once others had taken
+    # memory -- a synchronizing free + hipMalloc per launch)
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    first = []
+    for rnd in range(2):
+        for i, st in enumerate(streams):
+            ix.search_device(qry.data_ptr(), D * 4, NQ, oi.data_ptr(), od.data_ptr(), on.data_ptr(), None, k=10,
+                             epsilon=0.1, edge_size=0, seed_mode=SEED_GIVEN, d_seeds=d_seeds.data_ptr(),
+                             d_seed_off=d_soff.data_ptr(), stream=st.cuda_stream, visited_hash_log2=-2)
+            torch.cuda.synchronize()
+            slots = ix.last_search_slots()
+            assert slots >= 1
+            if rnd == 0:
+                first.append(slots)
+            else:
+                assert slots == first[i], (i, first, slots)
     ix.close()
     del rows
     torch.cuda.empty_cache()
