@@ -1129,6 +1129,8 @@ def main():
         if rank == 0:
             sl.pop("sweep", None)
             sl["scaling"] = "strong"
+            if "qg_form" in sl:
+                sl["qg_form"]["scaling"] = "strong"  # the same fixed index, the ranks share it
             sl["wall_s"] = time.time() - t0
             line["shard"] = sl
     if rank == 0:
