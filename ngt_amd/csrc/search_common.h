@@ -409,6 +409,29 @@ __device__ __forceinline__ uint32_t quad_sum_u32(uint32_t s) {
   return s;
 }
 
+// A lane's NW 8-byte code words of one row, fetched in 16-byte loads when
+// they are whole pairs (the row's lanes start 16-B aligned: 128-B code rows,
+// 32 B per lane): half the vector-memory instructions of 8-byte loads, each
+// touching the same rows' lines -- the per-instruction address work of the
+// texture unit, not the bytes, is what these gathers spend (TA busy 0.74 on
+// the C2 headline, profiles/r6t).
+template <int NW>
+__device__ __forceinline__ void load_code_words(const uint8_t* rowp, uint2 (&c)[NW]) {
+  if constexpr (NW % 2 == 0) {
+    const uint4* p = reinterpret_cast<const uint4*>(rowp);
+#pragma unroll
+    for (int w = 0; w < NW / 2; w++) {
+      const uint4 v = p[w];
+      c[2 * w] = make_uint2(v.x, v.y);
+      c[2 * w + 1] = make_uint2(v.z, v.w);
+    }
+  } else {
+    const uint2* p = reinterpret_cast<const uint2*>(rowp);
+#pragma unroll
+    for (int w = 0; w < NW; w++) c[w] = p[w];
+  }
+}
+
 template <int NCH>
 __device__ __forceinline__ void filter_l2u8(const uint8_t* qb, uint32_t sq, const uint8_t* codes,
                                             const uint32_t* ids, uint32_t* out, int m) {
@@ -427,9 +450,12 @@ __device__ __forceinline__ void filter_l2u8(const uint8_t* qb, uint32_t sq, cons
     for (int j = 0; j < 4; j++) {
       const int r = r0 + 16 * j + rs;
       const uint32_t id = r < m ? ids[r] : 0u;
-      const uint2* p = reinterpret_cast<const uint2*>(codes + (uint64_t)id * (4 * E)) + g * NW;
+      if (j == 0 || r0 + 16 * j < m) {
+        load_code_words<NW>(codes + (uint64_t)id * (4 * E) + g * (8 * NW), c[j]);
+      } else {
 #pragma unroll
-      for (int w = 0; w < NW; w++) c[j][w] = (j == 0 || r0 + 16 * j < m) ? p[w] : make_uint2(0u, 0u);
+        for (int w = 0; w < NW; w++) c[j][w] = make_uint2(0u, 0u);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {

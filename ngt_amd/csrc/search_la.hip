@@ -747,9 +747,7 @@ ngt_graph_search_la_kernel(SearchArgs a) {
                                           __HIP_MEMORY_SCOPE_AGENT);
             }
             // unconditional too (an empty entry reads object 0's codes)
-            const uint2* cp = reinterpret_cast<const uint2*>(a.fcodes + (uint64_t)id * (4 * E)) + g * NW;
-#pragma unroll
-            for (int w = 0; w < NW; w++) c[j][w] = cp[w];
+            load_code_words<NW>(a.fcodes + (uint64_t)id * (4 * E) + g * (8 * NW), c[j]);
           }
 #pragma unroll
           for (int j = 0; j < RG; j++) {
