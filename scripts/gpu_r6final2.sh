@@ -2,7 +2,7 @@
 # round 6 final (2), the tree as committed after the issue-bound fields: smoke,
 # the driver's bench command
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r6final2}; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; O=${1:-gpurun_out/r6final2}; case $O in gpurun_out/*) ;; *) O=gpurun_out/$O;; esac; mkdir -p $O
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log \
