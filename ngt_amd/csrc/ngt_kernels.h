@@ -180,6 +180,7 @@ struct ServeDevCtl {
   uint32_t claimed;  // tickets below this are taken by a worker
   uint32_t closing;  // the dispatcher has stopped: drain and leave
   uint32_t pad;      // why it stopped: 1 asked, 2 idle, 3 lifetime
+  uint32_t done;     // tickets answered (counted from the launch's first)
 };
 struct ServeArgs {
   const uint8_t* ring;     // [nring][req_bytes] pinned host memory
@@ -191,7 +192,7 @@ struct ServeArgs {
   const uint32_t* stop;    // pinned host words: [0] stop dispatching, [1] tickets handed out
   uint32_t start;          // first ticket of this launch
   uint32_t use_tree;       // seeds from the tree (else the request's)
-  uint64_t idle_ticks;     // dispatcher leaves after this long without a post (100 MHz clock)
+  uint64_t idle_ticks;     // dispatcher leaves after this long with nothing posted or in flight (100 MHz clock)
   uint64_t life_ticks;     // ... or this long in all; workers' own bound is longer
   TreeSeedArgs tree;
 };

@@ -107,8 +107,11 @@ __device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
 // ---- serving form (ngt_kernels.h ServeArgs) ---------------------------------
 // The dispatcher (one lane of block 0): publishes each ticket whose
 // request slot the host has posted, in ticket order, until the host asks it
-// to stop, nothing was posted for idle_ticks, or life_ticks have passed;
-// then tells the workers to drain.
+// to stop, nothing was posted or in flight for idle_ticks, or life_ticks have
+// passed; then tells the workers to drain.  The idle time counts from the
+// last answer, not the last post: a lone caller's search that outlasts
+// idle_ticks would otherwise close the grid under it, and its next call
+// would pay a relaunch.
 __device__ void serve_dispatch(const ServeArgs& sv) {
   if (lane_id() != 0) return;
   uint32_t avail = sv.start;
@@ -117,6 +120,8 @@ __device__ void serve_dispatch(const ServeArgs& sv) {
   uint32_t why = 0;  // 1 asked to stop, 2 idle, 3 lifetime
   for (;;) {
     const uint64_t now = wall_clock64();
+    // a posted ticket not answered yet: not idle
+    if (__hip_atomic_load(&sv.dctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != avail) last = now;
     if (__hip_atomic_load(sv.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) why = 1;
     // idle: nothing posted for idle_ticks and no ticket handed out unposted
     // (a caller between taking its ticket and posting it)
@@ -839,7 +844,10 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        if (lane == 0) __hip_atomic_store(&r->seq, qi + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) {
+          __hip_atomic_store(&r->seq, qi + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_add(&sv.dctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       } else {
         if ((uint32_t)lane < nres) {
           a.out_ids[(uint64_t)qi * k + lane] = key_id(rk);

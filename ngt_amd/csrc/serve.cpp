@@ -15,7 +15,9 @@
 //
 // Each caller polls its own response slot in host memory, so a query costs its
 // own search and nothing of anyone else's: no batch waits for its slowest
-// member.  The grid leaves when nothing was posted for idle_ms, after life_s,
+// member.  The grid leaves when nothing was posted or in flight for idle_ms
+// (a search longer than idle_ms keeps it: a sequential caller's next query
+// finds it running), after life_s,
 // or when asked (a configuration change, destroy); a caller that finds its
 // ticket unanswered with the grid gone launches the next grid, which starts at
 // the first unclaimed ticket.  The search is the batch kernel's (the same
@@ -23,7 +25,7 @@
 //
 //   NGT_AMD_SERVE=0             never serve (callers take the launch path)
 //   NGT_AMD_SERVE_WORKERS=n     worker workgroups, one query each (default: CUs - 1)
-//   NGT_AMD_SERVE_IDLE_MS=n     idle time before the grid leaves (default 20)
+//   NGT_AMD_SERVE_IDLE_MS=n     idle time (nothing posted or in flight) before the grid leaves (default 20)
 //   NGT_AMD_SERVE_LOG=1         a stderr line per grid: lifetime, why it left
 #include <float.h>
 #include <stdio.h>
@@ -173,7 +175,7 @@ int server_reap(Server* sv, bool ask) {
 
 // a grid for sv->cfg / sv->a (caller holds sv->mu; none running)
 int server_launch(ngt_amd_index* ix, Server* sv) {
-  ServeDevCtl c{sv->start, sv->start, 0u, 0u};
+  ServeDevCtl c{sv->start, sv->start, 0u, 0u, sv->start};
   HIP_OK(hipMemcpyAsync(sv->dctl.p, &c, sizeof c, hipMemcpyHostToDevice, sv->s));
   HIP_OK(hipStreamSynchronize(sv->s));
   __atomic_store_n(sv->stop, 0u, __ATOMIC_RELEASE);
