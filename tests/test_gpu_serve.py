@@ -114,6 +114,37 @@ def test_served_spill_and_slots(monkeypatch, knobs):
     ix.close()
 
 
+def test_grid_stays_while_a_search_runs(monkeypatch):
+    """The grid idles out only with nothing posted or in flight: with a 1 ms
+    idle time, sequential calls whose searches take longer than that (epsilon
+    1.0 over the whole 4k graph) are all answered by one grid -- the idle
+    time runs from the last answer, not the last post (serve.cpp,
+    search_lat.hip serve_dispatch) -- and equal the launch's answers."""
+    import time
+    monkeypatch.setenv("NGT_AMD_SERVE_IDLE_MS", "2")
+    ix, rows, offs, ids, tree = _anng()
+    rng = np.random.default_rng(23)
+    qs = rng.random((12, rows.shape[1]), dtype=np.float32)
+    ix.search_served(qs[0], k=10, epsilon=0.1, seed_mode=SEED_TREE)  # the grid is up
+    _, l0 = ix.serve_stats()
+    got, wall = [], []
+    for q in qs:
+        t = time.perf_counter()
+        got.append(ix.search_served(q, k=10, epsilon=1.0, seed_mode=SEED_TREE))
+        wall.append(time.perf_counter() - t)
+    _, l1 = ix.serve_stats()
+    assert all(g is not None for g in got)
+    assert min(wall) > 0.004, wall  # every search outlasts the idle time
+    assert l1 == l0, "grid launches during %d sequential calls: %d (call ms %s)" % (
+        len(qs), l1 - l0, [round(w * 1e3, 2) for w in wall])
+    bi, bd, bn, bc = ix.search(qs, k=10, epsilon=1.0, seed_mode=SEED_TREE)
+    for i, (gi, gd, gc) in enumerate(got):
+        assert list(gi) == list(bi[i, :bn[i]]), i
+        assert np.array_equal(gd.view(np.uint32), bd[i, :bn[i]].view(np.uint32)), i
+        assert gc[2] == bc[i, 2] and gc[2] > 200, (i, gc[2])  # long searches: hundreds of expansions
+    ix.close()
+
+
 def test_served_random_seeds_follow_the_rand_stream():
     """getRandomSeeds draws the same rand() stream whether the query is served
     or launched: after the same ngt_amd_srand both answer identically."""
