@@ -1052,6 +1052,10 @@ def main():
                 if si:
                     # the SIMDs' issue in measured (GRBM) cycles, scripts/pmc_clk.sh
                     line["roofline"]["counters"]["simd_issue"] = si
+                ta = tentry.get("texture_address")
+                if ta:
+                    # the texture address units' busy share over the same clock (PMC_TAG=ta pass)
+                    line["roofline"]["counters"]["texture_address"] = ta
                 line["roofline"]["bound"] = bound_from_counters(cn, ic_share(split, alg_bytes), si)
                 line["roofline"]["bound_note"] = (
                     "from the SQ counters and the byte split: 'issue' when the SIMDs issue in >= 0.7 of their "

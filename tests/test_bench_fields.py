@@ -80,3 +80,19 @@ def test_pick_expansion():
     # one below the target is skipped while another reaches it
     sw[3]["recall_at_10"] = 0.94
     assert bench.pick_expansion(sw, 0.95)["result_expansion"] == 3.0
+
+
+def test_traffic_entries_carry_clocked_passes():
+    """The four timed lines' traffic.json entries (the ones bench.py attaches
+    to C2, ANNG, qg and C3) hold both clocked counter passes: the SIMD issue
+    figures and the texture address units' busy share, each a fraction of
+    the GRBM-measured cycles."""
+    import json
+    import os
+    t = json.load(open(os.path.join(os.path.dirname(bench.__file__), "profiles", "traffic.json")))
+    clocked = [e for e in t["entries"] if "simd_issue" in e]
+    assert len(clocked) == 4
+    for e in clocked:
+        ta = e["texture_address"]
+        assert 0.0 < ta["ta_busy_frac"] < 1.0 and 0.0 < ta["vmem_per_cu_cycle"] < 1.0
+        assert 0.0 < e["simd_issue"]["simd_valu_util"] <= e["simd_issue"]["simd_issue_util"]
