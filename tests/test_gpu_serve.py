@@ -134,7 +134,7 @@ def test_grid_stays_while_a_search_runs(monkeypatch):
         wall.append(time.perf_counter() - t)
     _, l1 = ix.serve_stats()
     assert all(g is not None for g in got)
-    assert min(wall) > 0.004, wall  # every search outlasts the idle time
+    assert min(wall) > 0.003, wall  # every search outlasts the 2 ms idle time
     assert l1 == l0, "grid launches during %d sequential calls: %d (call ms %s)" % (
         len(qs), l1 - l0, [round(w * 1e3, 2) for w in wall])
     bi, bd, bn, bc = ix.search(qs, k=10, epsilon=1.0, seed_mode=SEED_TREE)
