@@ -717,6 +717,7 @@ static int run_search(ngt_amd_index* ix, SearchCtx* c, const ngt_amd_search_para
       b.lat_slots = cap <= 64 ? 32u : 16u;
       b.lat_tail = 4096u;
       b.lat_hop = lat_hop_default();
+      b.lat_feed = lat_feed_default();
       while (search_lat_lds_bytes(b) > lds_max && b.lat_tail > 512u) b.lat_tail -= 256u;
       while (search_lat_lds_bytes(b) > lds_max && b.lat_slots > 8u) b.lat_slots -= 2u;
       // test knobs: a small tail forces the HBM spill, few slots the orphan path

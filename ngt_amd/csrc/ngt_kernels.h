@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "knobs.h"
 
 namespace ngt_amd {
@@ -98,6 +100,7 @@ struct SearchArgs {
   uint32_t lat_slots;
   uint32_t lat_tail;
   uint32_t lat_hop;              // latency kernel: warm L2 for the nearest fresh neighbour of each list part
+  uint32_t lat_feed;             // latency kernel: head entries kept speculated (0: 16; capped by lat_slots)
   // launch schedule (ngt_amd_api.cpp run_search, "probe and resume"): the
   // w-th work item a slot claims is query order[w] (null: w), and a launch
   // has *nwork_dev work items (null: nq).  A probe launch (pause_after > 0)
@@ -216,6 +219,11 @@ inline int la_wpe() { return 4; }
 inline uint32_t lat_hop_default() {
   const char* e = ngt_amd::knob("NGT_AMD_LAT_HOP");
   return e ? (atoi(e) != 0 ? 1u : 0u) : 1u;
+}
+// latency kernel: head entries kept speculated; NGT_AMD_LAT_FEED=n (A/B)
+inline uint32_t lat_feed_default() {
+  const char* e = ngt_amd::knob("NGT_AMD_LAT_FEED");
+  return e ? (uint32_t)std::max(1, std::min(64, atoi(e))) : 0u;
 }
 uint32_t search_la_lds_bytes(const SearchArgs& a, int P);
 uint32_t search_lat_lds_bytes(const SearchArgs& a);

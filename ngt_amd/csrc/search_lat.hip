@@ -371,7 +371,8 @@ __global__ void __launch_bounds__(64 * W) ngt_graph_search_lat_kernel(SearchArgs
       uint64_t freem = nslots >= 64 ? ~0ull : ((1ull << nslots) - 1ull);  // free slots
       uint32_t sgen = 0u;  // lane s: slot s's issue generation (only this wave issues)
       uint64_t orphan = 0ull;                                             // issued, no longer in the head
-      const uint32_t F = nslots < 16u ? nslots : 16u;                     // head entries kept speculated
+      const uint32_t Fd = a.lat_feed ? a.lat_feed : 16u;
+      const uint32_t F = nslots < Fd ? nslots : Fd;                       // head entries kept speculated
 
       auto spill_push = [&](uint64_t key) {
         if (nspill >= a.spill_cap) {

@@ -253,6 +253,7 @@ int serve_args(ngt_amd_index* ix, const ngt_amd_search_params* prm, SearchArgs& 
   a.lat_slots = cap <= 64 ? 32u : 16u;
   a.lat_tail = 4096u;
   a.lat_hop = lat_hop_default();
+  a.lat_feed = lat_feed_default();
   while (search_lat_lds_bytes(a) > lds_max && a.lat_tail > 512u) a.lat_tail -= 256u;
   while (search_lat_lds_bytes(a) > lds_max && a.lat_slots > 8u) a.lat_slots -= 2u;
   if (const char* v = ngt_amd::knob("NGT_AMD_LAT_TAIL")) a.lat_tail = (uint32_t)std::max(128, std::min(4096, atoi(v)));
